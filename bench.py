@@ -1,0 +1,168 @@
+#!/usr/bin/env python
+"""Benchmark of the ray-trace hot path on MI355X: Mrays/s at 1920x1080 (BASELINE.json).
+
+Workload (BASELINE.json configs[2], the metric's 1920x1080 single-GPU config):
+excess_inputs/bunny.rti (4,968-triangle bunny + reflective floor +
+mirror spheres), 1920x1080, --bdepth 4.  A step renders frames of that scene through
+the C-ABI (librtamd.so); rays = traceRay calls (primary + reflection + refraction) +
+shadow rays, counted by the kernels and equal to the reference's counts.
+
+Multi-GPU (torchrun, one rank per GPU, RCCL): every frame is row-interleaved over all
+ranks (row r -> rank r mod N) and its RGB8 rows are gathered to rank 0 over xGMI; a
+step renders N frames, so per-GPU work is fixed (weak scaling).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3_bunny_1920x1080_bd4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cs184-raytracer_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+NODE_BYTES, TRI_BYTES, NRM_BYTES = 128, 72, 72   # SURVEY.md §8d algorithmic bytes
+RAY_IO_BYTES, PIXEL_BYTES = 64 + 64, 24
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="C3_bunny_1920x1080_bd4")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_round1.json"),
+                    help="PMC-measured HBM bytes per trace launch (rocprofv3 FETCH_SIZE/WRITE_SIZE), if present")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, w, h, bdepth, target_s):
+    """The CPU oracle (bit-exact restatement, the reference's brute-force algorithm and
+    2000-pixel block threading) on a bounded, evenly spaced row sample of the same frame."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(16, cores))
+    step = 270
+    while True:
+        t0 = time.perf_counter()
+        _, cnt = pyoracle.render(scene, w, h, bdepth=bdepth, threads=cores, rows=(step // 2, h, step))
+        dt = time.perf_counter() - t0
+        rays = cnt["trace_rays"] + cnt["shadow_rays"]
+        if dt * 2.5 > target_s or step <= 2:
+            rows = len(range(step // 2, h, step))
+            return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
+                    "sample": f"oracle/ (bit-exact CPU restatement, brute force) on {rows} rows "
+                              f"(every {step}th) of the same {w}x{h} frame: {rays} rays in {dt:.1f} s"}
+        step = max(2, int(step / max(2.0, min(8.0, target_s / max(dt, 1e-3) / 1.5))))
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+    import rtamd
+    from cases import CONFIGS, SCENES, option_kwargs
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    scene_rel, W, H, flags = CONFIGS[a.config]
+    kw = option_kwargs(flags)
+    scene = os.path.join(SCENES, scene_rel)
+    s = rtamd.load_scene(scene, device=local)
+    s.upload()
+    n_local = len(range(rank, H, world))
+    n_max = -(-H // world)
+    out = torch.empty((n_local, W, 3), dtype=torch.float64, device="cuda")
+    out8 = torch.zeros((n_max, W, 3), dtype=torch.uint8, device="cuda")
+    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rank, H, world)
+    stream = torch.cuda.current_stream().cuda_stream
+    gather = [torch.empty_like(out8) for _ in range(world)] if rank == 0 and world > 1 else None
+    frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+
+    totals = {"rays": 0, "kernel_ms": 0.0, "launches": 0, "bytes": 0}
+
+    def step(record):
+        for _ in range(world):  # N frames per step: per-GPU work fixed (weak scaling)
+            st = s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)
+            if world > 1:
+                dist.gather(out8, gather, dst=0)
+                if rank == 0:
+                    for r in range(world):
+                        frame[r::world] = gather[r][: len(range(r, H, world))]
+            elif rank == 0:
+                frame.copy_(out8[:H])
+            if record:
+                totals["rays"] += st.trace_rays + st.shadow_rays
+                totals["kernel_ms"] += st.kernel_ms
+                totals["launches"] += st.trace_launches
+                totals["bytes"] += ((st.trace_rays + st.shadow_rays) * RAY_IO_BYTES + st.node_visits * NODE_BYTES +
+                                    st.tri_tests * TRI_BYTES + st.candidates * NRM_BYTES + st.pixels * PIXEL_BYTES)
+
+    for _ in range(a.warmup):
+        step(False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    agg = torch.tensor([elapsed, float(totals["rays"]), totals["kernel_ms"], float(totals["launches"]),
+                        float(totals["bytes"])], dtype=torch.float64, device="cuda")
+    if world > 1:
+        t_max = agg[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
+        agg[0] = t_max[0]
+    elapsed, rays, kms, launches, nbytes = agg.tolist()
+    if rank == 0:
+        value = rays / elapsed / 1e6
+        achieved = (nbytes / launches) / ((kms / launches) * 1e-3) / 1e9 if launches else 0.0
+        traffic = None
+        if os.path.exists(a.traffic):
+            try:
+                traffic = json.load(open(a.traffic)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        res = {
+            "metric": "Mrays/s (primary+secondary) and wall-clock at 1920x1080; HBM GB/s vs peak",
+            "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic: shipped reference scene data (bunny.obj), "
+                                                        "deterministic, no RNG",
+            "config": {"workload": a.config, "scene": scene_rel, "width": W, "height": H,
+                       "bounce_depth": kw["bdepth"], "frames_per_step": world, "rays_per_frame": int(rays / a.steps / world),
+                       "ms_per_frame": round(elapsed / a.steps / world * 1e3, 3),
+                       "parallelism": f"row-interleaved x{world}, RCCL gather of RGB8 rows" if world > 1 else "1 GPU"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_trace", "avg_launch_ms": round(kms / launches, 4) if launches else None,
+                         "note": "algorithmic bytes per SURVEY.md §8d (ray I/O + LBVH nodes + triangles + normals "
+                                 "+ pixels), mostly L2-resident scene reads; see DESIGN.md"},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(scene, W, H, kw["bdepth"], a.cpu_seconds)
+        print(json.dumps(res), flush=True)
+    s.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,241 @@
+// Scene flattening + per-mesh LBVH construction (host).
+#include "bvh.h"
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include "xform.h"
+
+namespace rtamd {
+namespace {
+
+struct Box {
+	double lo[3], hi[3];
+	void empty() {
+		for (int k = 0; k < 3; k++) {
+			lo[k] = INFINITY;
+			hi[k] = -INFINITY;
+		}
+	}
+	void grow(const Box& b) {
+		for (int k = 0; k < 3; k++) {
+			lo[k] = std::min(lo[k], b.lo[k]);
+			hi[k] = std::max(hi[k], b.hi[k]);
+		}
+	}
+};
+
+// spread the low 21 bits of v to every third bit of a 63-bit word
+uint64_t spread3(uint64_t v) {
+	v &= 0x1fffff;
+	v = (v | v << 32) & 0x1f00000000ffffULL;
+	v = (v | v << 16) & 0x1f0000ff0000ffULL;
+	v = (v | v << 8) & 0x100f00f00f00f00fULL;
+	v = (v | v << 4) & 0x10c30c30c30c30c3ULL;
+	v = (v | v << 2) & 0x1249249249249249ULL;
+	return v;
+}
+
+struct Builder {
+	const std::vector<Box>& boxes;   // per face (mesh-local index)
+	std::vector<uint64_t> code;      // sorted Morton codes
+	std::vector<int32_t> order;      // sorted face indices
+	std::vector<DBvhNode>& nodes;
+	std::vector<int32_t> leaf_order; // faces in leaf order
+	double pad;
+	int max_depth = 0;
+	bool median_only = false;
+
+	struct Ref {
+		Box box;
+		int32_t first, count;  // count > 0: leaf
+	};
+
+	int split(int b, int e) const {  // [b, e) with e - b >= 2
+		if (median_only || code[b] == code[e - 1]) return (b + e) / 2;
+		const int prefix = __builtin_clzll(code[b] ^ code[e - 1]);
+		int lo = b, hi = e - 1;  // find last index sharing > prefix bits with code[b]
+		while (lo + 1 < hi) {
+			const int mid = (lo + hi) / 2;
+			if (__builtin_clzll(code[b] ^ code[mid]) > prefix)
+				lo = mid;
+			else
+				hi = mid;
+		}
+		return lo + 1;
+	}
+
+	Ref build(int b, int e, int depth) {
+		max_depth = std::max(max_depth, depth);
+		Ref r;
+		r.box.empty();
+		if (e - b <= kLeafFaces) {
+			r.first = static_cast<int32_t>(leaf_order.size());
+			r.count = e - b;
+			for (int i = b; i < e; i++) {
+				leaf_order.push_back(order[i]);
+				r.box.grow(boxes[order[i]]);
+			}
+			return r;
+		}
+		const int idx = static_cast<int>(nodes.size());
+		nodes.emplace_back();
+		const int m = split(b, e);
+		const Ref c[2] = {build(b, m, depth + 1), build(m, e, depth + 1)};
+		DBvhNode& n = nodes[idx];
+		std::memset(&n, 0, sizeof(n));
+		for (int k = 0; k < 2; k++) {
+			for (int a = 0; a < 3; a++) {
+				n.lo[k][a] = c[k].box.lo[a] - pad;
+				n.hi[k][a] = c[k].box.hi[a] + pad;
+			}
+			n.first[k] = c[k].first;
+			n.count[k] = c[k].count;
+			r.box.grow(c[k].box);
+		}
+		r.first = idx;
+		r.count = 0;
+		return r;
+	}
+};
+
+}  // namespace
+
+FlatScene flatten_scene(const Scene& s) {
+	FlatScene fs;
+	std::memset(&fs.camera, 0, sizeof(fs.camera));
+	if (s.has_camera) {
+		std::memcpy(fs.camera.eye, s.cam[0], sizeof(double) * 4);
+		std::memcpy(fs.camera.ll, s.cam[1], sizeof(double) * 4);
+		std::memcpy(fs.camera.lr, s.cam[2], sizeof(double) * 4);
+		std::memcpy(fs.camera.ul, s.cam[3], sizeof(double) * 4);
+		std::memcpy(fs.camera.ur, s.cam[4], sizeof(double) * 4);
+	}
+	for (const Light& l : s.lights) {
+		DLight d{};
+		for (int k = 0; k < 3; k++) {
+			d.color[k] = l.color[k];
+			d.vec[k] = l.vec[k];
+		}
+		d.falloff = l.falloff;
+		d.kind = l.kind;
+		fs.lights.push_back(d);
+	}
+	for (const Geometry& g : s.geoms) {
+		DGeom d{};
+		std::memcpy(d.fwd, g.fwd.m, sizeof(d.fwd));
+		std::memcpy(d.inv, g.inv.m, sizeof(d.inv));
+		d.kind = g.kind;
+		d.flip = g.det < 0;
+		d.bvh_root = -1;
+		DMaterial m{};
+		for (int k = 0; k < 3; k++) {
+			m.ka[k] = g.mat.ka[k];
+			m.kd[k] = g.mat.kd[k];
+			m.ks[k] = g.mat.ks[k];
+			m.kr[k] = g.mat.kr[k];
+			m.kt[k] = g.mat.kt[k];
+		}
+		m.ns = g.mat.ns;
+		m.ior = g.mat.ior;
+		m.kt_nonzero = !is_zero(g.mat.kt, 3);
+		m.kr_nonzero = !is_zero(g.mat.kr, 3);
+		d.mat = static_cast<int32_t>(fs.materials.size());
+		fs.materials.push_back(m);
+		if (g.kind == GEOM_SPHERE) {
+			for (int k = 0; k < 3; k++) d.center[k] = g.center[k];
+			const float rr = g.radius * g.radius;  // fp32 product, geometry.cpp:53
+			d.rr = static_cast<double>(rr);
+			fs.geoms.push_back(d);
+			continue;
+		}
+		// mesh
+		bool box_differs = false;
+		for (int k = 0; k < 4; k++) box_differs |= g.bb_min[k] != g.bb_max[k];
+		d.gate = box_differs && g.face_count > 1;
+		for (int k = 0; k < 3; k++) {
+			d.bb_min[k] = g.bb_min[k];
+			d.bb_max[k] = g.bb_max[k];
+		}
+		d.face_begin = static_cast<int32_t>(fs.face_geo.size());
+		d.face_count = static_cast<int32_t>(g.face_count);
+		auto emit = [&](int64_t local) {
+			const Face& f = s.faces[g.face_begin + local];
+			DFaceGeo fg{};
+			DFaceNrm fn{};
+			for (int k = 0; k < 3; k++) {
+				fg.p0[k] = f.p[0][k];
+				fg.va[k] = f.p[1][k] - f.p[0][k];  // face.points_[1] - face.points_[0] (geometry.cpp:80)
+				fg.vb[k] = f.p[2][k] - f.p[0][k];
+				fn.n0[k] = f.n[0][k];
+				fn.n1[k] = f.n[1][k];
+				fn.n2[k] = f.n[2][k];
+			}
+			fs.face_geo.push_back(fg);
+			fs.face_nrm.push_back(fn);
+			fs.face_id.push_back(static_cast<int32_t>(local));
+		};
+		if (g.face_count <= kLinearFaces) {
+			for (int64_t i = 0; i < g.face_count; i++) emit(i);
+			fs.geoms.push_back(d);
+			continue;
+		}
+		// LBVH over the object-space face boxes
+		std::vector<Box> boxes(g.face_count);
+		Box cb;
+		cb.empty();
+		double amax = 0;
+		for (int64_t i = 0; i < g.face_count; i++) {
+			const Face& f = s.faces[g.face_begin + i];
+			boxes[i].empty();
+			for (int v = 0; v < 3; v++)
+				for (int k = 0; k < 3; k++) {
+					boxes[i].lo[k] = std::min(boxes[i].lo[k], f.p[v][k]);
+					boxes[i].hi[k] = std::max(boxes[i].hi[k], f.p[v][k]);
+					amax = std::max(amax, std::fabs(f.p[v][k]));
+				}
+			Box c;
+			for (int k = 0; k < 3; k++) c.lo[k] = c.hi[k] = 0.5 * (boxes[i].lo[k] + boxes[i].hi[k]);
+			cb.grow(c);
+		}
+		std::vector<std::pair<uint64_t, int32_t>> keyed(g.face_count);
+		for (int64_t i = 0; i < g.face_count; i++) {
+			uint64_t q[3];
+			for (int k = 0; k < 3; k++) {
+				const double ext = cb.hi[k] - cb.lo[k];
+				const double c = 0.5 * (boxes[i].lo[k] + boxes[i].hi[k]);
+				double u = ext > 0 ? (c - cb.lo[k]) / ext : 0.5;
+				u = std::min(std::max(u, 0.0), 1.0);
+				q[k] = static_cast<uint64_t>(u * 2097151.0);
+			}
+			keyed[i] = {spread3(q[0]) << 2 | spread3(q[1]) << 1 | spread3(q[2]), static_cast<int32_t>(i)};
+		}
+		std::sort(keyed.begin(), keyed.end());
+		// Conservative padding: the traversal may prune a node only when no face inside it
+		// can pass the reference's Cramer test; 1e-9 of the largest coordinate magnitude is
+		// ~10^7 ulps of slack for the slab and Cramer rounding (validated bit-exact against
+		// the oracle over every shipped scene).
+		const double pad = 1e-9 * amax + 1e-300;
+		const size_t node_base = fs.nodes.size();
+		for (int attempt = 0; attempt < 2; attempt++) {
+			fs.nodes.resize(node_base);
+			Builder bld{boxes, {}, {}, fs.nodes, {}, pad};
+			bld.median_only = attempt == 1;
+			for (const auto& kv : keyed) {
+				bld.code.push_back(kv.first);
+				bld.order.push_back(kv.second);
+			}
+			bld.build(0, static_cast<int>(g.face_count), 0);
+			if (bld.max_depth + 2 >= kStackDepth && attempt == 0) continue;  // too deep: median splits
+			// inner-node indices are global (fs.nodes); leaf face indices are relative to the mesh
+			for (int32_t local : bld.leaf_order) emit(local);
+			fs.max_bvh_depth = std::max(fs.max_bvh_depth, bld.max_depth);
+			break;
+		}
+		d.bvh_root = static_cast<int32_t>(node_base);
+		fs.geoms.push_back(d);
+	}
+	return fs;
+}
+
+}  // namespace rtamd

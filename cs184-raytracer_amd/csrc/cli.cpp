@@ -1,0 +1,195 @@
+// rtamd — drop-in replacement for the reference's `as2` executable (main.cpp:40-85,
+// options.cpp:7-90): same flags (-o/--output, -t/--threads, -w/--width, -h/--height,
+// --bdepth, --intersection-only, positional .rti files), same messages and exit codes,
+// byte-identical PNG.  Adds --device N (HIP device) and --dump-raw FILE (f64 image).
+// The render itself runs on the GPU through the C-ABI (include/rtamd.h).
+#include <getopt.h>
+#include <signal.h>
+#include <sys/time.h>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <iostream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+#include "../../include/rtamd.h"
+
+namespace {
+
+struct Options {  // options.h:10-16 defaults
+	std::vector<std::string> inputs;
+	std::string output, dump_raw;
+	int threads = 1, width = 500, height = 500, bdepth = 10, device = 0;
+	bool intersection_only = false;
+};
+
+enum { OPT_HELP = 0, OPT_BDEPTH = 256, OPT_IO, OPT_DEVICE, OPT_DUMP };
+
+bool parse_int(const char* s, int& out) {
+	try {
+		out = std::stoi(s);
+		return true;
+	} catch (const std::logic_error&) {
+		return false;
+	}
+}
+
+bool parse_command_line(int argc, char** argv, Options& o) {  // options.cpp:18-86
+	static const struct option opts[] = {{"help", 0, nullptr, OPT_HELP},     {"output", 1, nullptr, 'o'},
+	                                     {"threads", 1, nullptr, 't'},       {"width", 1, nullptr, 'w'},
+	                                     {"height", 1, nullptr, 'h'},        {"bdepth", 1, nullptr, OPT_BDEPTH},
+	                                     {"intersection-only", 0, nullptr, OPT_IO},
+	                                     {"device", 1, nullptr, OPT_DEVICE}, {"dump-raw", 1, nullptr, OPT_DUMP},
+	                                     {nullptr, 0, nullptr, 0}};
+	int c;
+	while ((c = getopt_long(argc, argv, "t:w:h:o:", opts, nullptr)) != -1) {
+		switch (c) {
+			case 'o': o.output = optarg; break;
+			case OPT_IO: o.intersection_only = true; break;
+			case OPT_DUMP: o.dump_raw = optarg; break;
+			case 't':
+				if (!parse_int(optarg, o.threads)) {
+					std::cerr << "Error: Thread count is invalid." << std::endl;
+					return false;
+				}
+				if (o.threads <= 0) {
+					std::cerr << "Error: Thread count must be positive." << std::endl;
+					return false;
+				}
+				break;
+			case 'w':
+			case 'h': {
+				int& dest = c == 'w' ? o.width : o.height;
+				if (!parse_int(optarg, dest)) {
+					std::cerr << "Error: Width and/or height is invalid." << std::endl;
+					return false;
+				}
+				if (dest <= 0) {
+					std::cerr << "Error: Width and/or height must be positive." << std::endl;
+					return false;
+				}
+				break;
+			}
+			case OPT_BDEPTH:
+				if (!parse_int(optarg, o.bdepth)) {
+					std::cerr << "Error: Bounce depth is invalid." << std::endl;
+					return false;
+				}
+				if (o.bdepth < 0) {
+					std::cerr << "Error: Bounce depth must be non-negative." << std::endl;
+					return false;
+				}
+				break;
+			case OPT_DEVICE:
+				if (!parse_int(optarg, o.device) || o.device < 0) {
+					std::cerr << "Error: Device index is invalid." << std::endl;
+					return false;
+				}
+				break;
+			default:
+				std::cerr << "Usage: " << argv[0] << " [options] -o <output file> <input files>..." << std::endl;
+				return false;
+		}
+	}
+	while (optind < argc) o.inputs.push_back(argv[optind++]);
+	if (o.inputs.empty()) {
+		std::cerr << "Error: At least one input file must be specified." << std::endl;
+		return false;
+	}
+	if (o.output.empty()) {
+		std::cerr << "Error: An output file must be specified." << std::endl;
+		return false;
+	}
+	return true;
+}
+
+volatile sig_atomic_t g_progress_signaled = 0;
+void on_alarm(int) { g_progress_signaled = 1; }
+void set_alarm(bool enable) {  // main.cpp:28-38: 4 Hz progress tick
+	if (enable) signal(SIGALRM, on_alarm);
+	struct itimerval itv = {{0, 0}, {0, 0}};
+	itv.it_value.tv_usec = itv.it_interval.tv_usec = enable ? 1000000 / 4 : 0;
+	setitimer(ITIMER_REAL, &itv, nullptr);
+	if (!enable) signal(SIGALRM, SIG_DFL);
+}
+void update_progress(int complete, int total, void*) {  // main.cpp:12-22
+	if (complete != total && !g_progress_signaled) return;
+	std::putchar('\r');
+	std::printf("Rendering scene (%d/%d) (%.1f%%) ...", complete, total, 100.0 * complete / total);
+	std::fflush(stdout);
+	if (complete == total) std::putchar('\n');
+	g_progress_signaled = 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+	Options o;
+	if (!parse_command_line(argc, argv, o)) return 1;
+	if (!std::ofstream(o.output)) {  // main.cpp:45-51
+		std::cerr << "Error: Output file is not writable." << std::endl;
+		return 1;
+	}
+	std::remove(o.output.c_str());
+	rt_builder* b = rt_builder_create();
+	for (const std::string& f : o.inputs) {
+		const int rc = rt_builder_parse_rti(b, f.c_str());
+		std::cerr << rt_builder_warnings(b);
+		if (rc == RT_ERR_PARSE) {
+			std::cerr << "Error: " << rt_last_error() << std::endl;
+			return 1;
+		}
+		if (rc) {  // MathException escapes the reference's main (std::terminate)
+			std::cerr << "terminate called after throwing an instance of 'MathException'\n  what():  "
+			          << rt_last_error() << std::endl;
+			std::abort();
+		}
+	}
+	if (!rt_builder_has_camera(b)) {
+		std::cerr << "Error: At least one camera must be specified." << std::endl;
+		return 1;
+	}
+	rt_scene* scene = nullptr;
+	if (rt_scene_create(b, o.device, &scene)) {
+		std::cerr << "Error: " << rt_last_error() << std::endl;
+		return 1;
+	}
+	rt_render_params p{};
+	p.width = o.width;
+	p.height = o.height;
+	p.bounce_depth = o.bdepth;
+	p.intersection_only = o.intersection_only;
+	p.row_begin = 0;
+	p.row_end = o.height;
+	p.row_step = 1;
+	std::vector<double> img(static_cast<size_t>(o.width) * o.height * 3);
+	set_alarm(true);
+	const int rc = rt_render(scene, &p, img.data(), update_progress, nullptr, nullptr);
+	set_alarm(false);
+	if (rc == RT_ERR_MATH) {
+		std::cerr << "terminate called after throwing an instance of 'MathException'\n  what():  " << rt_last_error()
+		          << std::endl;
+		std::abort();
+	}
+	if (rc) {
+		std::cerr << "Error: " << rt_last_error() << std::endl;
+		return 1;
+	}
+	if (!o.dump_raw.empty()) {
+		FILE* f = std::fopen(o.dump_raw.c_str(), "wb");
+		if (f) {
+			std::fwrite(img.data(), sizeof(double), img.size(), f);
+			std::fclose(f);
+		}
+	}
+	std::vector<uint8_t> rgb(img.size());
+	rt_to_rgb8(img.data(), static_cast<int64_t>(o.width) * o.height, rgb.data());
+	if (rt_write_png(o.output.c_str(), rgb.data(), o.width, o.height)) {
+		std::cerr << "Error: " << rt_last_error() << std::endl;
+		return 1;
+	}
+	rt_scene_destroy(scene);
+	rt_builder_destroy(b);
+	return 0;
+}

@@ -1,0 +1,86 @@
+// Device-resident scene layout shared by the host uploader and the HIP kernels.
+//
+// HBM layout (all read-only after rt_scene_create):
+//   DGeom[G]        per-geometry record, insertion order (scene.cpp:147 loop order)
+//   DLight[L]       pre-transformed lights, definition order (scene.cpp:117)
+//   DFaceGeo[F]     per face: p0, va = p1-p0, vb = p2-p0 (object space)      80 B
+//   DFaceNrm[F]     per face: n0, n1, n2 (object space, w == 0 dropped)       80 B
+//   int32 face_id[F]  face index within its mesh in the reference's order (tie-break)
+//   DBvhNode[N]     flattened binary LBVH, child boxes stored in the parent   128 B
+// BVH meshes store their faces in LBVH leaf order; small meshes (<= kLinearFaces) keep
+// the reference's order and are scanned linearly exactly like geometry.cpp:78.
+#pragma once
+#include <cstdint>
+
+namespace rtamd {
+
+enum : int32_t { DGEOM_SPHERE = 0, DGEOM_MESH = 1 };
+enum : int32_t { DLIGHT_POINT = 0, DLIGHT_DIRECTIONAL = 1, DLIGHT_AMBIENT = 2 };
+
+constexpr int kLinearFaces = 8;   // meshes up to this size are scanned linearly (no BVH)
+constexpr int kLeafFaces = 4;     // faces per LBVH leaf
+constexpr int kStackDepth = 48;   // traversal stack entries per lane (LDS)
+
+struct alignas(16) DGeom {
+	double fwd[3][4];     // forwardTransform rows
+	double inv[3][4];     // inverseTransform rows
+	double center[3];     // sphere centre (w == 1 implied)
+	double rr;            // (double)(radius_ * radius_) with the product in fp32 (geometry.cpp:53)
+	double bb_min[3], bb_max[3];   // Mesh bounding box (object space) for the gate
+	int32_t kind;         // 0 sphere, 1 mesh
+	int32_t flip;         // transformDeterminant() < 0 (geometry.cpp:42-43)
+	int32_t gate;         // hitsBoundingBox gate active (geometry.cpp:72)
+	int32_t bvh_root;     // root node index, -1 = linear face scan
+	int32_t face_begin, face_count;
+	int32_t mat;          // index into DMaterial
+	int32_t pad;
+};
+
+struct alignas(16) DMaterial {   // rtbase.h:30-39
+	double ka[3], kd[3], ks[3], kr[3], kt[3];
+	double ns, ior;
+	int32_t kt_nonzero;   // !translucencyColor.isZero()  (scene.cpp:115)
+	int32_t kr_nonzero;   // !reflectiveColor.isZero()    (scene.cpp:130)
+};
+
+struct alignas(16) DLight {
+	double color[3];
+	double vec[3];        // point position or direction (both after the light's transform)
+	double falloff;
+	int32_t kind;         // 0 point, 1 directional, 2 ambient
+	int32_t pad;
+};
+
+struct alignas(16) DFaceGeo {
+	double p0[3], va[3], vb[3];
+	double pad;
+};
+
+struct alignas(16) DFaceNrm {
+	double n0[3], n1[3], n2[3];
+	double pad;
+};
+
+// child c of a node: leaf when count[c] > 0 (faces [first[c], first[c]+count[c])),
+// else inner node index first[c].  Boxes are padded outward (see bvh.cpp).
+struct alignas(16) DBvhNode {
+	double lo[2][3];
+	double hi[2][3];
+	int32_t first[2];
+	int32_t count[2];
+	double pad[2];
+};
+
+struct DCamera {
+	double eye[4], ll[4], lr[4], ul[4], ur[4];
+};
+
+// Device error codes -> MathException text (rtbase.h:14-22)
+enum DeviceError : int32_t {
+	DERR_NONE = 0,
+	DERR_NO_DIRECTION = 1,      // "ray has no direction"
+	DERR_POINT_DIRECTION = 2,   // "ray direction is a point vector"
+	DERR_STACK = 3,             // traversal stack overflow (internal)
+};
+
+}  // namespace rtamd

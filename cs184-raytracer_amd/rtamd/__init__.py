@@ -1,0 +1,318 @@
+"""rtamd — Python mirror of the reference's render interface over the C-ABI.
+
+The reference (gh2o/CS184-Raytracer) is a C++ program; its render path is driven by
+
+    Scene scene;                                   // scene.h:9-39
+    RTIParser(scene).parseFile(filename);          // parsers.cpp:93
+    scene.renderScene(image, progressHandler);     // scene.cpp:10-59
+    PNGWriter(filename).writeImage(image);         // writers.cpp:11-21
+
+with flags in the global ``programOptions`` (options.h:10-16).  This module exposes the
+same names over ``librtamd.so`` (include/rtamd.h), whose render runs as HIP kernels on
+an MI355X.  There is no CPU fallback: rendering without a HIP device raises
+``DeviceError`` (the CPU restatement under ``oracle/`` is test infrastructure only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librtamd.so")
+
+RT_OK, RT_ERR_PARSE, RT_ERR_MATH, RT_ERR_ARG, RT_ERR_DEVICE, RT_ERR_IO = 0, -1, -2, -3, -4, -5
+
+
+class RTError(RuntimeError):
+    """Base class of rtamd errors."""
+
+
+class ParseException(RTError):
+    """ParseException (exceptions.h:6-21)."""
+
+
+class MathException(RTError):
+    """MathException (exceptions.h:23-26): what() text of the reference."""
+
+
+class WriteException(RTError):
+    """WriteException (exceptions.h:28-31)."""
+
+
+class DeviceError(RTError):
+    """HIP runtime failure or no HIP device."""
+
+
+class ArgumentError(RTError, ValueError):
+    pass
+
+
+class rt_render_params(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("bounce_depth", ctypes.c_int32),
+                ("intersection_only", ctypes.c_int32), ("row_begin", ctypes.c_int32), ("row_end", ctypes.c_int32),
+                ("row_step", ctypes.c_int32), ("chunk_pixels", ctypes.c_int32)]
+
+
+class rt_counters(ctypes.Structure):
+    _fields_ = [("trace_rays", ctypes.c_int64), ("shadow_rays", ctypes.c_int64), ("reflect_rays", ctypes.c_int64),
+                ("refract_rays", ctypes.c_int64), ("pixels", ctypes.c_int64), ("intersection_max", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double), ("levels", ctypes.c_int32), ("trace_launches", ctypes.c_int32),
+                ("node_visits", ctypes.c_int64), ("tri_tests", ctypes.c_int64), ("candidates", ctypes.c_int64),
+                ("sphere_tests", ctypes.c_int64)]
+
+
+class rt_scene_info(ctypes.Structure):
+    _fields_ = [("n_geometries", ctypes.c_int32), ("n_spheres", ctypes.c_int32), ("n_meshes", ctypes.c_int32),
+                ("n_lights", ctypes.c_int32), ("n_faces", ctypes.c_int64), ("n_bvh_nodes", ctypes.c_int64),
+                ("device_bytes", ctypes.c_int64)]
+
+
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Loads librtamd.so (built in-tree by ``make -C cs184-raytracer_amd``); fails loudly."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C cs184-raytracer_amd` "
+                          "(or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, cp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "rt_builder_create": (vp, []),
+        "rt_builder_destroy": (None, [vp]),
+        "rt_builder_parse_rti": (i32, [vp, cp]),
+        "rt_builder_has_camera": (i32, [vp]),
+        "rt_builder_warnings": (cp, [vp]),
+        "rt_scene_create": (i32, [vp, i32, ctypes.POINTER(vp)]),
+        "rt_scene_destroy": (None, [vp]),
+        "rt_scene_get_info": (i32, [vp, ctypes.POINTER(rt_scene_info)]),
+        "rt_render": (i32, [vp, ctypes.POINTER(rt_render_params), vp, PROGRESS_FN, vp, ctypes.POINTER(rt_counters)]),
+        "rt_render_device": (i32, [vp, ctypes.POINTER(rt_render_params), vp, vp, vp, ctypes.POINTER(rt_counters)]),
+        "rt_normalize_device": (i32, [vp, vp, i64, dbl, vp, vp]),
+        "rt_to_rgb8": (None, [vp, i64, vp]),
+        "rt_write_png": (i32, [cp, vp, i32, i32]),
+        "rt_last_error": (cp, []),
+        "rt_version": (cp, []),
+        "rt_device_count": (i32, []),
+        "rt_selftest_math": (i32, [i32, i32, vp, vp, vp, i64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _raise(rc: int, what: str = "") -> None:
+    if rc == RT_OK:
+        return
+    msg = lib().rt_last_error().decode(errors="replace")
+    cls = {RT_ERR_PARSE: ParseException, RT_ERR_MATH: MathException, RT_ERR_ARG: ArgumentError,
+           RT_ERR_DEVICE: DeviceError, RT_ERR_IO: WriteException}.get(rc, RTError)
+    raise cls(msg or what)
+
+
+@dataclass
+class Options:
+    """Options (options.h:10-16); ``programOptions`` below is the module-wide instance."""
+    inputFilenames_: List[str] = field(default_factory=list)
+    outputFilename_: str = ""
+    renderThreadsCount_: int = 1
+    renderWidth_: int = 500
+    renderHeight_: int = 500
+    bounceDepth_: int = 10
+    intersectionOnly_: bool = False
+
+
+programOptions = Options()
+
+
+@dataclass
+class RenderStats:
+    trace_rays: int
+    shadow_rays: int
+    reflect_rays: int
+    refract_rays: int
+    pixels: int
+    intersection_max: float
+    kernel_ms: float
+    levels: int
+    trace_launches: int
+    node_visits: int
+    tri_tests: int
+    candidates: int
+    sphere_tests: int
+
+    @property
+    def rays(self) -> int:
+        """Rays in the Mrays/s metric: traceRay calls + shadow rays."""
+        return self.trace_rays + self.shadow_rays
+
+
+def _stats(c: rt_counters) -> RenderStats:
+    return RenderStats(c.trace_rays, c.shadow_rays, c.reflect_rays, c.refract_rays, c.pixels, c.intersection_max,
+                       c.kernel_ms, c.levels, c.trace_launches, c.node_visits, c.tri_tests, c.candidates,
+                       c.sphere_tests)
+
+
+class Scene:
+    """Scene (scene.h:9-39): accumulates parsed files; uploads to HBM on first render."""
+
+    def __init__(self, device: int = 0):
+        self._b = lib().rt_builder_create()
+        self._scene = None
+        self.device = device
+        self.last_stats: Optional[RenderStats] = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def close(self) -> None:
+        if getattr(self, "_scene", None):
+            lib().rt_scene_destroy(self._scene)
+            self._scene = None
+        if getattr(self, "_b", None):
+            lib().rt_builder_destroy(self._b)
+            self._b = None
+
+    def hasCamera(self) -> bool:  # scene.h:20
+        return bool(lib().rt_builder_has_camera(self._b))
+
+    def warnings(self) -> str:
+        return lib().rt_builder_warnings(self._b).decode()
+
+    def _parse(self, filename: str) -> None:
+        if self._scene:
+            raise ArgumentError("scene already uploaded; parse all files before rendering")
+        _raise(lib().rt_builder_parse_rti(self._b, os.fsencode(filename)))
+
+    def upload(self) -> None:
+        """rt_scene_create: build the LBVHs and upload the scene to the device once."""
+        if self._scene:
+            return
+        p = ctypes.c_void_p()
+        _raise(lib().rt_scene_create(self._b, self.device, ctypes.byref(p)))
+        self._scene = p
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        self.upload()
+        return self._scene
+
+    def info(self) -> rt_scene_info:
+        i = rt_scene_info()
+        _raise(lib().rt_scene_get_info(self.handle, ctypes.byref(i)))
+        return i
+
+    def params(self, width: int, height: int, bounce_depth: int, intersection_only: bool, row_begin: int = 0,
+               row_end: Optional[int] = None, row_step: int = 1, chunk_pixels: int = 0) -> rt_render_params:
+        return rt_render_params(width, height, bounce_depth, int(bool(intersection_only)), row_begin,
+                                height if row_end is None else row_end, row_step, chunk_pixels)
+
+    def renderScene(self, output: Optional[np.ndarray] = None,
+                    phandler: Optional[Callable[[int, int], None]] = None, options: Optional[Options] = None,
+                    rows: Optional[tuple] = None, chunk_pixels: int = 0) -> np.ndarray:
+        """Scene::renderScene (scene.cpp:10-59).
+
+        ``output`` is the RasterImage: float64 array of shape (H, W, 3), caller-owned (allocated
+        here from ``options`` when None).  ``rows = (begin, end, step)`` renders a row-interleaved
+        subset into an (n_rows, W, 3) array (multi-GPU partition).
+        """
+        o = options or programOptions
+        W, H = o.renderWidth_, o.renderHeight_
+        rb, re_, rs = rows if rows is not None else (0, H, 1)
+        n_rows = max(0, -(-(re_ - rb) // rs))
+        if output is None:
+            output = np.empty((n_rows, W, 3), dtype=np.float64)
+        if output.dtype != np.float64 or output.shape != (n_rows, W, 3) or not output.flags.c_contiguous:
+            raise ArgumentError(f"output must be a C-contiguous float64 array of shape {(n_rows, W, 3)}")
+        prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels)
+        cb = PROGRESS_FN((lambda c, t, u: phandler(c, t)) if phandler else (lambda c, t, u: None))
+        cnt = rt_counters()
+        _raise(lib().rt_render(self.handle, ctypes.byref(prm), output.ctypes.data_as(ctypes.c_void_p), cb, None,
+                               ctypes.byref(cnt)))
+        self.last_stats = _stats(cnt)
+        return output
+
+    def render_device(self, params: rt_render_params, out_rgb_ptr: int = 0, out_rgb8_ptr: int = 0,
+                      stream_ptr: int = 0) -> RenderStats:
+        """rt_render_device into device buffers (e.g. torch tensors' data_ptr())."""
+        cnt = rt_counters()
+        _raise(lib().rt_render_device(self.handle, ctypes.byref(params), out_rgb_ptr or None, out_rgb8_ptr or None,
+                                      stream_ptr or None, ctypes.byref(cnt)))
+        self.last_stats = _stats(cnt)
+        return self.last_stats
+
+    def normalize_device(self, rgb_ptr: int, n_pixels: int, max_value: float, out_rgb8_ptr: int = 0,
+                         stream_ptr: int = 0) -> None:
+        _raise(lib().rt_normalize_device(self.handle, rgb_ptr, n_pixels, max_value, out_rgb8_ptr or None,
+                                         stream_ptr or None))
+
+
+class RTIParser:
+    """RTIParser (parsers.h:5-47): one instance per file, transform/material restart."""
+
+    def __init__(self, scene: Scene):
+        self.scene = scene
+
+    def parseFile(self, filename: str) -> None:
+        self.scene._parse(filename)
+
+
+def to_rgb8(image: np.ndarray) -> np.ndarray:
+    """PNGWriter::convertToRGBImage (writers.cpp:4-9)."""
+    img = np.ascontiguousarray(image, dtype=np.float64)
+    out = np.empty(img.shape, dtype=np.uint8)
+    lib().rt_to_rgb8(img.ctypes.data_as(ctypes.c_void_p), img.size // 3, out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+class PNGWriter:
+    """PNGWriter (writers.h:5-16): byte-identical to libpng 1.6.13's simplified writer."""
+
+    def __init__(self, filename: str):
+        self.filename = filename
+
+    def writeImage(self, image: np.ndarray) -> None:
+        rgb = image if image.dtype == np.uint8 else to_rgb8(image)
+        rgb = np.ascontiguousarray(rgb)
+        h, w = rgb.shape[0], rgb.shape[1]
+        _raise(lib().rt_write_png(os.fsencode(self.filename), rgb.ctypes.data_as(ctypes.c_void_p), w, h))
+
+
+def device_count() -> int:
+    return int(lib().rt_device_count())
+
+
+def selftest_math(op: str, x: np.ndarray, y: Optional[np.ndarray] = None, device: int = 0) -> np.ndarray:
+    """Runs the kernels' device pow/sqrt/div on the GPU for comparison with the host libm."""
+    code = {"pow": 0, "sqrt": 1, "div": 2}[op]
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    yy = np.ascontiguousarray(y if y is not None else x, dtype=np.float64)
+    out = np.empty_like(x)
+    _raise(lib().rt_selftest_math(device, code, x.ctypes.data_as(ctypes.c_void_p), yy.ctypes.data_as(ctypes.c_void_p),
+                                  out.ctypes.data_as(ctypes.c_void_p), x.size))
+    return out
+
+
+def load_scene(files, device: int = 0) -> Scene:
+    """main.cpp:53-66: one RTIParser per file, camera required."""
+    s = Scene(device)
+    for f in ([files] if isinstance(files, (str, os.PathLike)) else files):
+        RTIParser(s).parseFile(str(f))
+    if not s.hasCamera():
+        raise ArgumentError("At least one camera must be specified.")
+    return s

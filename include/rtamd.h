@@ -1,0 +1,140 @@
+/*
+ * rtamd — MI355X-native Whitted ray tracer: the C-ABI drop-in boundary.
+ *
+ * Replaces the render path of gh2o/CS184-Raytracer (reference at /root/reference):
+ *
+ *   reference                                         this ABI
+ *   ------------------------------------------------  ------------------------------------------
+ *   Scene scene;                     main.cpp:53       rt_builder_create
+ *   RTIParser(scene).parseFile(f)    parsers.cpp:93    rt_builder_parse_rti   (+ OBJParser, :253)
+ *   scene.hasCamera()                scene.h:20        rt_builder_has_camera
+ *   (geometry/lights live in Scene)  scene.h:35-38     rt_scene_create        (upload once to HBM)
+ *   Scene::renderScene(img, ph)      scene.h:14,       rt_render              (host f64 image)
+ *                                    scene.cpp:10-59   rt_render_device       (device buffers)
+ *   ProgressHandler(int,int)         scene.h:12        rt_progress_fn (+ user pointer)
+ *   programOptions.bounceDepth_ ...  options.h:10-16   rt_render_params
+ *   PNGWriter(f).writeImage(img)     writers.cpp:11-21 rt_write_png           (byte-identical PNG)
+ *   convertToRGBImage                writers.cpp:4-9   rt_to_rgb8
+ *   MathException / ParseException  exceptions.h      return codes + rt_last_error()
+ *
+ * Plain pointers and sizes only; no HIP or torch types.  Images are row-major
+ * H x W x 3 (the RasterImage layout, scene.h:11).  All functions return RT_OK (0) or
+ * a negative RT_ERR_* code; rt_last_error() then holds the message text, identical to
+ * the reference's exception what() where the reference throws.
+ */
+#ifndef RTAMD_H
+#define RTAMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+	RT_OK = 0,
+	RT_ERR_PARSE = -1,   /* ParseException (exceptions.h:6-21): "line N: ..." / "file not found: ..." */
+	RT_ERR_MATH = -2,    /* MathException (exceptions.h:23-26): "ray has no direction", ...          */
+	RT_ERR_ARG = -3,     /* invalid argument (sizes, rows, null pointers)                            */
+	RT_ERR_DEVICE = -4,  /* HIP runtime failure, or the HIP path is unavailable                      */
+	RT_ERR_IO = -5       /* WriteException (exceptions.h:28-31) / output not writable                */
+};
+
+/* ---------------------------------------------------------------- ingest (host C++) */
+typedef struct rt_builder rt_builder;
+
+rt_builder* rt_builder_create(void);
+void rt_builder_destroy(rt_builder* b);
+/* One call = one `RTIParser parser(scene); parser.parseFile(path);` (main.cpp:54-62):
+ * transform and material state restart for every file, geometry/lights accumulate. */
+int rt_builder_parse_rti(rt_builder* b, const char* path);
+int rt_builder_has_camera(const rt_builder* b);
+/* Warnings printed by the reference (ParseException::showWarning), "Warning: ...\n" each. */
+const char* rt_builder_warnings(const rt_builder* b);
+
+typedef struct rt_scene_info {
+	int32_t n_geometries, n_spheres, n_meshes, n_lights;
+	int64_t n_faces;         /* triangles incl. the two faces of every `tri` line      */
+	int64_t n_bvh_nodes;     /* flattened LBVH nodes over all meshes                  */
+	int64_t device_bytes;    /* HBM held by the uploaded scene                        */
+} rt_scene_info;
+
+/* ---------------------------------------------------------------- device scene */
+typedef struct rt_scene rt_scene;
+
+/* Builds the per-mesh LBVHs and uploads geometry, materials, lights and camera to
+ * HBM of HIP device `device` once; the scene is immutable afterwards. */
+int rt_scene_create(const rt_builder* b, int device, rt_scene** out);
+void rt_scene_destroy(rt_scene* s);
+int rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
+
+/* ---------------------------------------------------------------- render */
+typedef void (*rt_progress_fn)(int complete, int total, void* user);
+
+typedef struct rt_render_params {
+	int32_t width, height;        /* -w / -h (options.h:13-14)                             */
+	int32_t bounce_depth;         /* --bdepth (options.h:15), >= 0                         */
+	int32_t intersection_only;    /* --intersection-only (options.h:16)                    */
+	/* Rows rendered: row_begin, row_begin+row_step, ... < row_end (row-interleaved
+	 * multi-GPU partition).  {0, height, 1} renders the whole image. */
+	int32_t row_begin, row_end, row_step;
+	/* Pixels per wavefront pass (bounds queue memory); 0 = automatic. */
+	int32_t chunk_pixels;
+} rt_render_params;
+
+typedef struct rt_counters {
+	int64_t trace_rays;      /* Scene::traceRay calls: primary + reflection + refraction */
+	int64_t shadow_rays;     /* shadow castRay calls (scene.cpp:90-91)                   */
+	int64_t reflect_rays, refract_rays;
+	int64_t pixels;
+	double  intersection_max;   /* max over rendered pixels of maxCoeff (scene.cpp:50-53),
+	                               only with intersection_only                          */
+	double  kernel_ms;          /* summed device time of the trace kernels (HIP events) */
+	int32_t levels;             /* wavefront levels executed (max over chunks)          */
+	int32_t trace_launches;     /* trace-kernel launches (levels summed over chunks)    */
+	/* work done by the trace kernels (algorithmic bytes/flops) */
+	int64_t node_visits;        /* LBVH nodes visited (2 child boxes tested each)       */
+	int64_t tri_tests;          /* ray-triangle (Cramer) tests                          */
+	int64_t candidates;         /* tests that reached the normal fetch + facing test    */
+	int64_t sphere_tests;       /* ray-sphere tests                                     */
+} rt_counters;
+
+/* Scene::renderScene into a caller-owned host buffer of n_rows*W*3 doubles
+ * (n_rows = rows selected by row_begin/row_end/row_step, in that order).
+ * With intersection_only and the whole image selected, the output is normalised by
+ * the global maximum exactly as scene.cpp:50-58; otherwise the raw 1/d^2 values are
+ * returned with counters->intersection_max for the caller's global reduction. */
+int rt_render(rt_scene* s, const rt_render_params* p, double* out_rgb,
+              rt_progress_fn progress, void* user, rt_counters* counters);
+
+/* Same, with outputs in device memory (either may be NULL): out_rgb_dev (n_rows*W*3
+ * doubles) and out_rgb8_dev (n_rows*W*3 bytes, writers.cpp:4-9 quantisation fused).
+ * `stream` is a hipStream_t (NULL = the scene's own stream); the call returns when
+ * the work on it is complete. */
+int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev,
+                     uint8_t* out_rgb8_dev, void* stream, rt_counters* counters);
+
+/* In-place scale of a device f64 image by 1/max (the --intersection-only tail of
+ * scene.cpp:56, Color3d /= scalar == multiply by the reciprocal) + optional rgb8. */
+int rt_normalize_device(rt_scene* s, double* rgb_dev, int64_t n_pixels, double max_value,
+                        uint8_t* out_rgb8_dev, void* stream);
+
+/* ---------------------------------------------------------------- output */
+/* writers.cpp:4-9: clamp to [0,1], *255, truncate (NaN -> 0). */
+void rt_to_rgb8(const double* rgb, int64_t n_pixels, uint8_t* out);
+/* PNGWriter::writeImage (writers.cpp:11-21) byte for byte: libpng 1.6.13 simplified
+ * write of 8-bit RGB, sRGB chunk, libpng's filter heuristic, zlib level 6 Z_FILTERED. */
+int rt_write_png(const char* path, const uint8_t* rgb, int width, int height);
+
+/* ---------------------------------------------------------------- diagnostics */
+const char* rt_last_error(void);
+const char* rt_version(void);
+int rt_device_count(void);
+/* Device math self-test: out[i] = pow(x[i], y[i]), sqrt(x[i]), x[i]/y[i] computed by the
+ * kernels' own device routines (op 0 = pow, 1 = sqrt, 2 = div) for host comparison. */
+int rt_selftest_math(int device, int op, const double* x, const double* y, double* out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTAMD_H */

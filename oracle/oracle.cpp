@@ -662,7 +662,8 @@ Ray viewingRay(const SceneData& s, double rF, double cF) {  // rtbase.h:74-84
 }  // namespace
 
 extern "C" int oracle_render(const char* const* files, int n_files, int W, int H, int bdepth, int intersection_only,
-                             int threads, int row_begin, int row_end, double* out, oracle_counters* counters) {
+                             int threads, int row_begin, int row_end, int row_step, double* out,
+                             oracle_counters* counters) {
 	g_last_error.clear();
 	g_warnings.clear();
 	SceneData scene;
@@ -679,13 +680,14 @@ extern "C" int oracle_render(const char* const* files, int n_files, int W, int H
 		g_last_error = "At least one camera must be specified.";
 		return 1;
 	}
-	if (W <= 0 || H <= 0 || row_begin < 0 || row_end > H || row_begin > row_end) {
+	if (W <= 0 || H <= 0 || row_begin < 0 || row_end > H || row_begin > row_end || row_step <= 0) {
 		g_last_error = "bad image geometry";
 		return 3;
 	}
-	const int64_t first = (int64_t)row_begin * W, total = (int64_t)row_end * W;
+	const int64_t n_rows = (row_end - row_begin + row_step - 1) / row_step;
+	const int64_t total = n_rows * W;  // selected pixels, dispensed in 2000-pixel blocks
 	const int64_t block = 2000;  // scene.cpp:13
-	std::atomic<int64_t> next(first);
+	std::atomic<int64_t> next(0);
 	std::mutex mu;
 	Counters sum;
 	std::string err;
@@ -697,11 +699,11 @@ extern "C" int oracle_render(const char* const* files, int n_files, int W, int H
 				if (start >= total) break;
 				int64_t end = std::min(start + block, total);
 				for (int64_t i = start; i < end; i++) {
-					int r = (int)(i / W), c = (int)(i % W);
+					int r = row_begin + (int)(i / W) * row_step, c = (int)(i % W);
 					double rF = (r + 0.5) / H;  // scene.cpp:28-29
 					double cF = (c + 0.5) / W;
 					C3 v = t.traceRay(viewingRay(scene, rF, cF), bdepth, false);
-					double* o = out + (i - first) * 3;
+					double* o = out + i * 3;
 					o[0] = v.r; o[1] = v.g; o[2] = v.b;
 				}
 			}
@@ -721,7 +723,7 @@ extern "C" int oracle_render(const char* const* files, int n_files, int W, int H
 		g_last_error = err;
 		return 2;
 	}
-	if (intersection_only && row_begin == 0 && row_end == H) {  // scene.cpp:50-58
+	if (intersection_only && row_begin == 0 && row_end == H && row_step == 1) {  // scene.cpp:50-58
 		double mx = std::numeric_limits<double>::min();
 		for (int64_t i = 0; i < total; i++)
 			mx = std::max(mx, std::max(std::max(out[i * 3], out[i * 3 + 1]), out[i * 3 + 2]));

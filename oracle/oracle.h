@@ -24,15 +24,15 @@ typedef struct oracle_counters {
 	int64_t face_tests;      // faces visited in the linear face loop, geometry.cpp:78
 } oracle_counters;
 
-// Renders rows [row_begin, row_end) of an H x W image of the scene made of the given
+// Renders rows row_begin, row_begin+row_step, ... < row_end of an H x W image of the scene made of the given
 // .rti files (main.cpp:54-62: one parser per file), with bounce depth `bdepth` and the
-// --intersection-only flag.  out: (row_end-row_begin)*W*3 doubles, row-major.
+// --intersection-only flag.  out: n_rows*W*3 doubles, row-major (selected rows in order).
 // intersection-only normalisation (scene.cpp:50-58) is applied over the rendered rows
 // only when they cover the whole image.  threads: std::threads with the reference's
 // 2000-pixel block dispenser (scene.cpp:13-48, with the last block clamped).
 // Returns 0, or 1 = parse error, 2 = math error (text in oracle_last_error()).
 int oracle_render(const char* const* rti_files, int n_files, int W, int H, int bdepth,
-                  int intersection_only, int threads, int row_begin, int row_end,
+                  int intersection_only, int threads, int row_begin, int row_end, int row_step,
                   double* out, oracle_counters* counters);
 const char* oracle_last_error(void);
 // Warnings the parser printed (ParseException::showWarning text, exceptions.h:15-17),

@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
 	for (int i = optind; i < argc; i++) files.push_back(argv[i]);
 	std::vector<double> img((size_t)W * H * 3);
 	oracle_counters cnt;
-	int rc = oracle_render(files.data(), (int)files.size(), W, H, bdepth, io, T, 0, H, img.data(), &cnt);
+	int rc = oracle_render(files.data(), (int)files.size(), W, H, bdepth, io, T, 0, H, 1, img.data(), &cnt);
 	std::fputs(oracle_last_warnings(), stderr);
 	if (rc) {
 		std::fprintf(stderr, "Error: %s\n", oracle_last_error());
