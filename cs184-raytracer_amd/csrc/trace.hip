@@ -16,6 +16,7 @@
 //   invT * n       (M0k n0 + M2k n2) + (M1k n1 + M3k n3)
 //   normalized()   division by the norm; normalize() multiplies by the reciprocal
 #include "trace.h"
+#include "glibc_pow.h"
 #include <cmath>
 
 namespace rtamd {
@@ -365,7 +366,7 @@ __global__ void __launch_bounds__(kBlock) k_trace(DeviceScene S, FrameGeometry f
 				int dummy_g;
 				V3 dP, dN;
 				if (cast_ray<true>(S, P, Ld, lrev ^ inside, dL, dummy_d, dummy_g, dP, dN, stack, ctr, ws)) continue;
-				const double fall = point ? pow(dL, -L.falloff) : 1.0;
+				const double fall = point ? glibc_pow(dL, -L.falloff) : 1.0;
 				double att[3];
 #pragma unroll
 				for (int k = 0; k < 3; k++) att[k] = point ? fall * L.color[k] : L.color[k];
@@ -373,7 +374,7 @@ __global__ void __launch_bounds__(kBlock) k_trace(DeviceScene S, FrameGeometry f
 #pragma unroll
 				for (int k = 0; k < 3; k++) col[k] = col[k] + (diff * att[k]) * M.kd[k];
 				const V3 R = (2 * nl) * N - Ld;
-				const double spec = pow(max0(-dot4z(d, R)), M.ns);
+				const double spec = glibc_pow(max0(-dot4z(d, R)), M.ns);
 #pragma unroll
 				for (int k = 0; k < 3; k++) col[k] = col[k] + (spec * att[k]) * M.ks[k];
 			}
@@ -533,7 +534,7 @@ __global__ void k_selftest(int op, const double* x, const double* y, double* out
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
 	if (op == 0)
-		out[i] = pow(x[i], y[i]);
+		out[i] = glibc_pow(x[i], y[i]);
 	else if (op == 1)
 		out[i] = sqrt(x[i]);
 	else

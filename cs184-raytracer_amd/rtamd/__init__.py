@@ -84,6 +84,12 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} is missing: build it with `make -C cs184-raytracer_amd` "
                           "(or __graft_entry__.build())")
+    try:
+        # One HIP runtime per process: when PyTorch is present its libamdhip64.so.7 must be
+        # the one librtamd binds to (same soname), so torch buffers/streams/RCCL interoperate.
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, cp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
     sig = {
