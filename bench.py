@@ -91,19 +91,14 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     gather = [torch.empty_like(out8) for _ in range(world)] if rank == 0 and world > 1 else None
     frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    from rtamd import dist as rd
 
     totals = {"rays": 0, "kernel_ms": 0.0, "launches": 0, "bytes": 0}
 
     def step(record):
         for _ in range(world):  # N frames per step: per-GPU work fixed (weak scaling)
             st = s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)
-            if world > 1:
-                dist.gather(out8, gather, dst=0)
-                if rank == 0:
-                    for r in range(world):
-                        frame[r::world] = gather[r][: len(range(r, H, world))]
-            elif rank == 0:
-                frame.copy_(out8[:H])
+            rd.gather_rows(out8, H, dst=0, out=frame, bufs=gather)  # RCCL gather of RGB8 rows
             if record:
                 totals["rays"] += st.trace_rays + st.shadow_rays
                 totals["kernel_ms"] += st.kernel_ms

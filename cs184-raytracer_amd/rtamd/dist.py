@@ -1,0 +1,79 @@
+"""Multi-GPU frame partition for the render path: one process per GPU, RCCL over xGMI.
+
+The reference renders one image with a thread pool over 2000-pixel blocks
+(scene.cpp:13-48).  Here a frame is split row-interleaved over the ranks (row r is
+rendered by rank r mod N: the costly glass/mirror regions of a frame are spread evenly),
+each rank renders its rows on its own GPU (scene replicated in every GPU's HBM), and the
+RGB8 rows are gathered to rank 0 — the only data-path exchange.  --intersection-only
+needs one more collective: the reference normalises by the maximum over the whole image
+(scene.cpp:50-58), so ranks all-reduce (MAX) their local maxima first.
+
+The helpers take torch tensors (CUDA tensors with the "nccl" backend = RCCL, CPU tensors
+with "gloo"), so the same code is exercised by the CPU tests.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def rank_rows(height: int, rank: int, world: int) -> Tuple[int, int, int]:
+    """(row_begin, row_end, row_step) of this rank's rows."""
+    return rank, height, world
+
+
+def n_rows(height: int, rank: int, world: int) -> int:
+    return len(range(rank, height, world))
+
+
+def global_max(value: float, device: torch.device) -> float:
+    """All-reduce MAX of a scalar (the --intersection-only normaliser)."""
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
+                out: Optional[torch.Tensor] = None, bufs: Optional[list] = None) -> Optional[torch.Tensor]:
+    """Gathers every rank's interleaved rows (n_local, W, C) into a (H, W, C) frame on `dst`."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if world == 1:
+        if out is None:
+            return local.clone()
+        out.copy_(local)
+        return out
+    n_max = -(-height // world)
+    if local.shape[0] != n_max:
+        pad = torch.zeros((n_max,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad[: local.shape[0]] = local
+        local = pad
+    if rank == dst:
+        if bufs is None:
+            bufs = [torch.empty_like(local) for _ in range(world)]
+        dist.gather(local, bufs, dst=dst)
+        if out is None:
+            out = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        for r in range(world):
+            out[r::world] = bufs[r][: n_rows(height, r, world)]
+        return out
+    dist.gather(local, None, dst=dst)
+    return None
+
+
+def render_frame(render_rows: Callable[[Tuple[int, int, int]], Tuple[torch.Tensor, float]], height: int,
+                 intersection_only: bool, device: torch.device, dst: int = 0) -> Optional[torch.Tensor]:
+    """Distributed Scene::renderScene: returns the (H, W, 3) float64 frame on `dst`.
+
+    render_rows(rows) renders this rank's rows and returns (float64 (n_local, W, 3), local max).
+    """
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    img, local_max = render_rows(rank_rows(height, rank, world))
+    if intersection_only:
+        m = global_max(max(local_max, 2.2250738585072014e-308), device)  # max init DBL_MIN (scene.cpp:51)
+        img.mul_(1.0 / m)  # Color3d /= scalar multiplies by the reciprocal
+    return gather_rows(img, height, dst)

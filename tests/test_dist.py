@@ -1,0 +1,60 @@
+"""Row-interleaved multi-rank partition + gather (rtamd.dist), world_size 2 over gloo on CPU.
+
+The per-rank renderer here is the CPU oracle (test infrastructure); on GPUs the same
+rtamd.dist code runs with the "nccl" (RCCL) backend and the HIP renderer (bench.py).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from cases import SCENES
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, scene, w, h, bdepth, io, q):
+    import torch.distributed as dist
+    import pyoracle
+    from rtamd import dist as rd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def render_rows(rows):
+            img, _ = pyoracle.render(scene, w, h, bdepth=bdepth, intersection_only=io, threads=2, rows=rows)
+            local_max = float(np.nanmax(img)) if img.size else 0.0
+            return torch.from_numpy(img), local_max
+        frame = rd.render_frame(render_rows, h, io, torch.device("cpu"))
+        if rank == 0:
+            q.put(frame.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("scene,io", [("excess_inputs/refraction3.rti", False), ("inputs/input-02.rti", True),
+                                      ("inputs/input-09.rti", False)])
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_frame_equals_single_render(oracle, scene, io, world):
+    w, h, bdepth = 33, 23, 4
+    path = os.path.join(SCENES, scene)
+    want, _ = oracle.render(path, w, h, bdepth=bdepth, intersection_only=io)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, w, h, bdepth, io, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert np.array_equal(got, want)

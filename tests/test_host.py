@@ -1,0 +1,103 @@
+"""Host-side (CPU) checks of librtamd: ABI exports, PNG writer, ingest, pow restatement, CLI.
+
+No GPU is needed: these load librtamd.so and call only its host functions.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from cases import REPO, SCENES, SHIPPED, scene_files
+
+HEADER = os.path.join(REPO, "include", "rtamd.h")
+CLI = os.path.join(REPO, "cs184-raytracer_amd", "bin", "rtamd")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(rt_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_library_exports_every_declared_function(rt):
+    names = declared_functions()
+    assert len(names) >= 17
+    for n in names:
+        assert hasattr(rt.lib(), n), f"{n} declared in include/rtamd.h but not exported"
+
+
+@pytest.mark.parametrize("png", sorted(SHIPPED))
+def test_png_writer_is_byte_identical_to_libpng(rt, tmp_path, png):
+    from PIL import Image
+    ref = os.path.join(REPO, "tests", "golden", "shipped", png)
+    rgb = np.ascontiguousarray(np.asarray(Image.open(ref).convert("RGB")))
+    out = tmp_path / png
+    rt.PNGWriter(str(out)).writeImage(rgb)
+    assert out.read_bytes() == open(ref, "rb").read()
+
+
+def test_png_writer_small_images_use_reduced_window(rt, tmp_path):
+    """Images <= 16 KiB take libpng's windowBits reduction + CMF rewrite (pngwutil.c:251-288,370-385)."""
+    from PIL import Image
+    for w, h in [(1, 1), (7, 5), (40, 30), (73, 74)]:
+        rgb = (np.arange(w * h * 3, dtype=np.uint32).reshape(h, w, 3) * 37 % 251).astype(np.uint8)
+        out = tmp_path / f"s{w}x{h}.png"
+        rt.PNGWriter(str(out)).writeImage(rgb)
+        assert np.array_equal(np.asarray(Image.open(out).convert("RGB")), rgb)
+
+
+def test_to_rgb8_matches_writer_conversion(rt, oracle):
+    rng = np.random.default_rng(0)
+    v = np.concatenate([rng.normal(0.5, 0.7, 30000), [np.nan, np.inf, -np.inf, 0.0, -0.0, 1.0, 255 / 255]])
+    v = np.resize(v, (v.size // 3) * 3).reshape(-1, 1, 3)
+    assert np.array_equal(rt.to_rgb8(v), oracle.to_rgb8(v))
+
+
+@pytest.mark.parametrize("scene", scene_files())
+def test_ingest_errors_and_warnings_match_oracle(rt, oracle, scene):
+    path = os.path.join(SCENES, scene)
+    s = rt.Scene()
+    err = None
+    try:
+        rt.RTIParser(s).parseFile(path)
+    except rt.RTError as e:
+        err = str(e)
+    try:
+        oracle.render(path, 2, 2, bdepth=0)
+        oerr = None
+    except oracle.OracleError as e:
+        oerr = str(e)
+    assert err == oerr
+    assert s.warnings() == oracle.warnings()
+    if err is None:
+        assert s.hasCamera()
+
+
+def test_pow_restatement_matches_libm(tmp_path):
+    exe = tmp_path / "pow_check"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off",
+                    "-I" + os.path.join(REPO, "cs184-raytracer_amd", "csrc"),
+                    os.path.join(REPO, "tests", "native", "pow_check.cpp"), "-o", str(exe)], check=True)
+    p = subprocess.run([str(exe), "2000000"], capture_output=True, text=True)
+    assert p.returncode == 0, p.stdout
+
+
+@pytest.mark.parametrize("args,msg", [
+    ([], "Error: At least one input file must be specified."),
+    (["x.rti"], "Error: An output file must be specified."),
+    (["-o", "/tmp/x.png", "-w", "abc", "x.rti"], "Error: Width and/or height is invalid."),
+    (["-o", "/tmp/x.png", "-h", "0", "x.rti"], "Error: Width and/or height must be positive."),
+    (["-o", "/tmp/x.png", "-t", "-2", "x.rti"], "Error: Thread count must be positive."),
+    (["-o", "/tmp/x.png", "--bdepth", "-1", "x.rti"], "Error: Bounce depth must be non-negative."),
+    (["-o", "/nonexistent_dir/x.png", "x.rti"], "Error: Output file is not writable."),
+    (["-o", "/tmp/rtamd_cli_test.png", "/nonexistent.rti"], "Error: file not found: /nonexistent.rti"),
+])
+def test_cli_option_errors_match_reference(args, msg):
+    """options.cpp:18-86 / main.cpp:40-66 messages and exit status 1 (checked before any GPU use)."""
+    if not os.path.exists(CLI):
+        pytest.skip("CLI not built")
+    p = subprocess.run([CLI] + args, capture_output=True, text=True)
+    assert p.returncode == 1
+    assert msg in p.stderr
