@@ -41,28 +41,51 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(scene, w, h, bdepth, target_s):
-    """The CPU oracle (bit-exact restatement, the reference's brute-force algorithm and
-    2000-pixel block threading) on a bounded, evenly spaced row sample of the same frame."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import pyoracle
+def _cores():
     try:
-        cores = len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(16, cores))
-    step = 270
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the GPU box's CPU share is 16
+
+
+def cpu_baseline(s, scene, w, h, bdepth, target_s):
+    """CPU leg on this host's cores over a bounded, evenly spaced row sample of the same frame.
+
+    Prefers the UNMODIFIED reference (oracle/_ref/refharness, built from /root/reference/src
+    by `make -C oracle ref`; its fork-parallel pixel loop = one reference process per core);
+    falls back to the bit-exact CPU restatement oracle/ (\"port\").  Rays in the sample are
+    the kernels' counts for the same rows (equal to the reference's, see tests)."""
+    import subprocess
+    import rtamd
+    cores = _cores()
+    harness = os.path.join(REPO, "oracle", "_ref", "refharness")
+    kind = "reference" if os.access(harness, os.X_OK) else "port"
+    step = 90
     while True:
-        t0 = time.perf_counter()
-        _, cnt = pyoracle.render(scene, w, h, bdepth=bdepth, threads=cores, rows=(step // 2, h, step))
-        dt = time.perf_counter() - t0
-        rays = cnt["trace_rays"] + cnt["shadow_rays"]
-        if dt * 2.5 > target_s or step <= 2:
-            rows = len(range(step // 2, h, step))
-            return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
-                    "sample": f"oracle/ (bit-exact CPU restatement, brute force) on {rows} rows "
-                              f"(every {step}th) of the same {w}x{h} frame: {rays} rays in {dt:.1f} s"}
-        step = max(2, int(step / max(2.0, min(8.0, target_s / max(dt, 1e-3) / 1.5))))
+        rows = (step // 2, h, step)
+        if kind == "reference":
+            env = dict(os.environ, RT_REF_ROWS="%d:%d:%d" % rows)
+            t0 = time.perf_counter()
+            subprocess.run([harness, scene, "-o", "/dev/null", "-w", str(w), "-h", str(h), "--bdepth", str(bdepth),
+                            "-t", str(cores)], env=env, check=True, capture_output=True)
+            dt = time.perf_counter() - t0
+        else:
+            sys.path.insert(0, os.path.join(REPO, "oracle"))
+            import pyoracle
+            t0 = time.perf_counter()
+            pyoracle.render(scene, w, h, bdepth=bdepth, threads=cores, rows=rows)
+            dt = time.perf_counter() - t0
+        s.renderScene(options=rtamd.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth), rows=rows)
+        rays = s.last_stats.rays
+        n = len(range(*rows))
+        if dt * 2.5 > target_s or step <= 1:
+            what = ("unmodified reference (oracle/_ref/refharness, %d worker processes)" % cores if kind == "reference"
+                    else "oracle/ CPU restatement (%d threads)" % cores)
+            return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": cores, "kind": kind,
+                    "sample": f"{what}, brute-force face loop, on {n} rows (every {step}th) of the same {w}x{h} "
+                              f"frame: {rays} rays in {dt:.1f} s wall (incl. scene parse)"}
+        step = max(1, int(step / max(2.0, min(8.0, target_s / max(dt, 1e-3) / 1.5))))
 
 
 def main():
@@ -93,7 +116,8 @@ def main():
     frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     from rtamd import dist as rd
 
-    totals = {"rays": 0, "kernel_ms": 0.0, "launches": 0, "bytes": 0}
+    totals = {"rays": 0, "ms": [0.0, 0.0, 0.0], "launches": [0, 0, 0], "bytes": [0, 0, 0]}
+    work = {}
 
     def step(record):
         for _ in range(world):  # N frames per step: per-GPU work fixed (weak scaling)
@@ -101,10 +125,17 @@ def main():
             rd.gather_rows(out8, H, dst=0, out=frame, bufs=gather)  # RCCL gather of RGB8 rows
             if record:
                 totals["rays"] += st.trace_rays + st.shadow_rays
-                totals["kernel_ms"] += st.kernel_ms
-                totals["launches"] += st.trace_launches
-                totals["bytes"] += ((st.trace_rays + st.shadow_rays) * RAY_IO_BYTES + st.node_visits * NODE_BYTES +
-                                    st.tri_tests * TRI_BYTES + st.candidates * NRM_BYTES + st.pixels * PIXEL_BYTES)
+                for k in range(3):
+                    totals["ms"][k] += st.stage_ms[k]
+                    totals["launches"][k] += st.stage_launches[k]
+                # SURVEY.md §8d algorithmic bytes, attributed to the kernel that moves them
+                for k, nrays in ((0, st.trace_rays), (1, st.shadow_rays)):
+                    totals["bytes"][k] += (nrays * RAY_IO_BYTES + st.stage_node_visits[k] * NODE_BYTES +
+                                           st.stage_tri_tests[k] * TRI_BYTES + st.stage_candidates[k] * NRM_BYTES)
+                totals["bytes"][2] += st.pixels * PIXEL_BYTES
+                work.update({"trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
+                             "node_visits": list(st.stage_node_visits), "tri_tests": list(st.stage_tri_tests),
+                             "candidates": list(st.stage_candidates), "sphere_tests": list(st.stage_sphere_tests)})
 
     for _ in range(a.warmup):
         step(False)
@@ -118,21 +149,25 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    agg = torch.tensor([elapsed, float(totals["rays"]), totals["kernel_ms"], float(totals["launches"]),
-                        float(totals["bytes"])], dtype=torch.float64, device="cuda")
+    agg = torch.tensor([elapsed, float(totals["rays"])] + totals["ms"] + [float(x) for x in totals["launches"]] +
+                       [float(x) for x in totals["bytes"]], dtype=torch.float64, device="cuda")
     if world > 1:
         t_max = agg[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
         dist.all_reduce(agg, op=dist.ReduceOp.SUM)
         agg[0] = t_max[0]
-    elapsed, rays, kms, launches, nbytes = agg.tolist()
+    v = agg.tolist()
+    elapsed, rays, stage_ms, stage_launches, stage_bytes = v[0], v[1], v[2:5], v[5:8], v[8:11]
     if rank == 0:
         value = rays / elapsed / 1e6
+        names = ["k_closest", "k_shadow", "k_shade"]
+        dom = max(range(3), key=lambda k: stage_ms[k])  # the dominant kernel
+        kms, launches, nbytes = stage_ms[dom], stage_launches[dom], stage_bytes[dom]
         achieved = (nbytes / launches) / ((kms / launches) * 1e-3) / 1e9 if launches else 0.0
         traffic = None
         if os.path.exists(a.traffic):
             try:
-                traffic = json.load(open(a.traffic)).get("hbm_bytes_per_launch")
+                traffic = json.load(open(a.traffic)).get("hbm_bytes_per_launch", {}).get(names[dom])
             except Exception:
                 traffic = None
         res = {
@@ -147,12 +182,17 @@ def main():
                        "parallelism": f"row-interleaved x{world}, RCCL gather of RGB8 rows" if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_trace", "avg_launch_ms": round(kms / launches, 4) if launches else None,
-                         "note": "algorithmic bytes per SURVEY.md §8d (ray I/O + LBVH nodes + triangles + normals "
-                                 "+ pixels), mostly L2-resident scene reads; see DESIGN.md"},
+                         "kernel": names[dom], "avg_launch_ms": round(kms / launches, 4) if launches else None,
+                         "note": "algorithmic bytes per SURVEY.md §8d (ray I/O + LBVH nodes + triangles + normals), "
+                                 "mostly L2-resident scene reads; see DESIGN.md",
+                         "stages": {names[k]: {"ms_per_frame": round(stage_ms[k] / a.steps / world, 4),
+                                               "launches_per_frame": stage_launches[k] / a.steps / world,
+                                               "GBps": round(stage_bytes[k] / (stage_ms[k] * 1e-3) / 1e9, 1)
+                                               if stage_ms[k] else None} for k in range(3)},
+                         "work_per_frame_rank0": work},
         }
         if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(scene, W, H, kw["bdepth"], a.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(s, scene, W, H, kw["bdepth"], a.cpu_seconds)
         print(json.dumps(res), flush=True)
     s.close()
     if world > 1:

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -58,9 +59,12 @@ struct rt_scene {
 	std::vector<LevelBuffers> levels;
 	rtamd::DeviceCounters* ctr = nullptr;        // device
 	rtamd::DeviceCounters* ctr_host = nullptr;   // pinned mirror
+	unsigned long long* stats = nullptr;         // device, kStatShards x kStatStride
+	std::vector<unsigned long long> stats_host;
 	double* out_dev = nullptr;                   // staging for rt_render
 	int64_t out_capacity = 0;
-	hipEvent_t ev_begin = nullptr, ev_end = nullptr;
+	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // level stage boundaries
+	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketShadow0;  // measured best on C3
 };
 
 namespace {
@@ -91,9 +95,11 @@ int ensure_level(rt_scene* s, size_t level, int64_t capacity) {
 	}
 	capacity = std::max<int64_t>(capacity, 1024);
 	const int64_t n = capacity;
-	// 12 double arrays + 2 int32 arrays + 1 byte array, each 256-B aligned
+	const int64_t nl = std::max(8, s->ds.occl_stride);
+	// 18 double arrays, 4 int32 arrays, inside flags and n x lights shadow verdicts,
+	// each 256-B aligned
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	const int64_t bytes = 12 * align(n * 8) + 2 * align(n * 4) + align(n);
+	const int64_t bytes = 18 * align(n * 8) + 4 * align(n * 4) + align(n) + align(n * nl);
 	HIP_TRY(hipMalloc(&L.block, bytes));
 	char* p = static_cast<char*>(L.block);
 	auto take = [&](int64_t b) {
@@ -101,12 +107,15 @@ int ensure_level(rt_scene* s, size_t level, int64_t capacity) {
 		p += align(b);
 		return r;
 	};
-	double** d[12] = {&L.lv.ox, &L.lv.oy, &L.lv.oz, &L.lv.dx, &L.lv.dy, &L.lv.dz,
-	                  &L.lv.cr, &L.lv.cg, &L.lv.cb, &L.lv.kr, &L.lv.kg, &L.lv.kb};
+	double** d[18] = {&L.lv.ox, &L.lv.oy, &L.lv.oz, &L.lv.dx, &L.lv.dy, &L.lv.dz, &L.lv.hpx, &L.lv.hpy, &L.lv.hpz,
+	                  &L.lv.hnx, &L.lv.hny, &L.lv.hnz, &L.lv.cr, &L.lv.cg, &L.lv.cb, &L.lv.kr, &L.lv.kg, &L.lv.kb};
 	for (double** q : d) *q = reinterpret_cast<double*>(take(n * 8));
+	L.lv.hgeom = reinterpret_cast<int32_t*>(take(n * 4));
+	L.lv.hit_list = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.child_refr = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.child_refl = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.inside = reinterpret_cast<uint8_t*>(take(n));
+	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.capacity = capacity;
 	return RT_OK;
 }
@@ -170,9 +179,9 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
 	std::unique_ptr<rt_scene> s(new rt_scene());
 	s->device = device;
+	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);  // tuning knob
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-	HIP_TRY(hipEventCreate(&s->ev_begin));
-	HIP_TRY(hipEventCreate(&s->ev_end));
+	for (hipEvent_t& e : s->ev) HIP_TRY(hipEventCreate(&e));
 	int rc;
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
@@ -185,12 +194,25 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	s->ds.n_nonambient = 0;
-	for (const auto& l : fs.lights) s->ds.n_nonambient += l.kind != rtamd::LIGHT_AMBIENT;
+	for (size_t li = 0; li < fs.lights.size(); li++) {
+		if (fs.lights[li].kind == rtamd::LIGHT_AMBIENT) continue;
+		if (s->ds.n_nonambient >= rtamd::kMaxShadowLights) {
+			rt_scene_destroy(s.release());
+			return fail(RT_ERR_ARG, "too many non-ambient lights (max 64)");
+		}
+		s->ds.shadow_light[s->ds.n_nonambient++] = static_cast<int32_t>(li);
+	}
+	s->ds.occl_stride = (s->ds.n_nonambient + 7) / 8 * 8;
 	void* c = nullptr;
 	HIP_TRY(hipMalloc(&c, sizeof(rtamd::DeviceCounters)));
 	s->allocs.push_back(c);
 	s->ctr = static_cast<rtamd::DeviceCounters*>(c);
 	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->ctr_host), sizeof(rtamd::DeviceCounters), hipHostMallocDefault));
+	void* st = nullptr;
+	HIP_TRY(hipMalloc(&st, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
+	s->allocs.push_back(st);
+	s->stats = static_cast<unsigned long long*>(st);
+	s->stats_host.resize(rtamd::kStatShards * rtamd::kStatStride);
 	rt_scene_info& in = s->info;
 	in.n_geometries = s->ds.n_geoms;
 	for (const auto& g : fs.geoms) (g.kind == rtamd::GEOM_SPHERE ? in.n_spheres : in.n_meshes)++;
@@ -210,8 +232,8 @@ void rt_scene_destroy(rt_scene* s) {
 	for (void* p : s->allocs) (void)hipFree(p);
 	if (s->out_dev) (void)hipFree(s->out_dev);
 	if (s->ctr_host) (void)hipHostFree(s->ctr_host);
-	if (s->ev_begin) (void)hipEventDestroy(s->ev_begin);
-	if (s->ev_end) (void)hipEventDestroy(s->ev_end);
+	for (hipEvent_t e : s->ev)
+		if (e) (void)hipEventDestroy(e);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
 	delete s;
 }
@@ -236,9 +258,8 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 	const int64_t chunk_rows = std::max<int64_t>(1, chunk_pixels / W);
 	rt_counters cnt{};
 	cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
-	rtamd::DeviceCounters zero{};
-	zero.max_bits = 0;
-	HIP_TRY(hipMemcpyAsync(s->ctr, &zero, sizeof(zero), hipMemcpyHostToDevice, st));
+	HIP_TRY(hipMemsetAsync(s->ctr, 0, sizeof(rtamd::DeviceCounters), st));
+	HIP_TRY(hipMemsetAsync(s->stats, 0, sizeof(unsigned long long) * s->stats_host.size(), st));
 	std::vector<int64_t> level_n;
 	float kernel_ms_total = 0.f;
 	for (int64_t r0 = 0; r0 < n_rows; r0 += chunk_rows) {
@@ -259,15 +280,16 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 			if (remaining > 0 && (rc = ensure_level(s, L + 1, 2 * n))) return rc;
 			HIP_TRY(hipMemsetAsync(&s->ctr->next_count, 0, sizeof(int32_t), st));
 			const rtamd::RayLevel& next = remaining > 0 ? s->levels[L + 1].lv : s->levels[L].lv;
-			HIP_TRY(hipEventRecord(s->ev_begin, st));
-			HIP_TRY(rtamd::launch_trace_level(s->ds, fg, L, n, remaining, s->levels[L].lv, next, s->ctr, st));
-			HIP_TRY(hipEventRecord(s->ev_end, st));
+			HIP_TRY(rtamd::launch_level(s->ds, fg, L, n, remaining, s->levels[L].lv, next, s->ctr, s->stats, st,
+			                            s->ev, cnt.stage_launches, s->packet_mask));
 			HIP_TRY(hipMemcpyAsync(s->ctr_host, s->ctr, sizeof(rtamd::DeviceCounters), hipMemcpyDeviceToHost, st));
 			HIP_TRY(hipStreamSynchronize(st));
-			float ms = 0.f;
-			HIP_TRY(hipEventElapsedTime(&ms, s->ev_begin, s->ev_end));
-			kernel_ms_total += ms;
-			cnt.trace_launches++;
+			for (int k = 0; k < 3; k++) {
+				float ms = 0.f;
+				HIP_TRY(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
+				cnt.stage_ms[k] += ms;
+				kernel_ms_total += ms;
+			}
 			if (s->ctr_host->error) break;
 			cnt.trace_rays += n;
 			const int64_t nn = s->ctr_host->next_count;
@@ -278,23 +300,39 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		for (int L = static_cast<int>(level_n.size()) - 2; L >= 0; L--)
 			HIP_TRY(rtamd::launch_reduce_level(level_n[L], s->levels[L].lv, s->levels[L + 1].lv, st));
 		HIP_TRY(rtamd::launch_output(n0, s->levels[0].lv, out_rgb_dev ? out_rgb_dev + r0 * W * 3 : nullptr,
-		                             out_rgb8_dev ? out_rgb8_dev + r0 * W * 3 : nullptr, io, s->ctr, st));
+		                             out_rgb8_dev ? out_rgb8_dev + r0 * W * 3 : nullptr, io, s->stats, st));
 		cnt.levels = std::max<int32_t>(cnt.levels, static_cast<int32_t>(level_n.size()));
 		cnt.pixels += n0;
 	}
 	HIP_TRY(hipMemcpyAsync(s->ctr_host, s->ctr, sizeof(rtamd::DeviceCounters), hipMemcpyDeviceToHost, st));
 	HIP_TRY(hipStreamSynchronize(st));
 	if (s->ctr_host->error) return fail(RT_ERR_MATH, device_error_text(s->ctr_host->error));
-	cnt.shadow_rays = static_cast<int64_t>(s->ctr_host->hits) * s->ds.n_nonambient;
-	cnt.reflect_rays = static_cast<int64_t>(s->ctr_host->refl);
-	cnt.refract_rays = static_cast<int64_t>(s->ctr_host->refr);
-	cnt.node_visits = static_cast<int64_t>(s->ctr_host->node_visits);
-	cnt.tri_tests = static_cast<int64_t>(s->ctr_host->tri_tests);
-	cnt.candidates = static_cast<int64_t>(s->ctr_host->candidates);
-	cnt.sphere_tests = static_cast<int64_t>(s->ctr_host->sphere_tests);
-	if (io && s->ctr_host->max_bits) {
+	HIP_TRY(hipMemcpy(s->stats_host.data(), s->stats, sizeof(unsigned long long) * s->stats_host.size(),
+	                  hipMemcpyDeviceToHost));
+	unsigned long long sum[rtamd::ST_COUNT] = {0};
+	for (int sh = 0; sh < rtamd::kStatShards; sh++)
+		for (int k = 0; k < rtamd::ST_COUNT; k++) {
+			const unsigned long long v = s->stats_host[sh * rtamd::kStatStride + k];
+			sum[k] = (k == rtamd::ST_MAX_BITS) ? std::max(sum[k], v) : sum[k] + v;
+		}
+	cnt.shadow_rays = static_cast<int64_t>(sum[rtamd::ST_HITS]) * s->ds.n_nonambient;
+	cnt.reflect_rays = static_cast<int64_t>(sum[rtamd::ST_REFL]);
+	cnt.refract_rays = static_cast<int64_t>(sum[rtamd::ST_REFR]);
+	for (int k = 0; k < 2; k++) {
+		const int b = k ? rtamd::ST_NODES1 : rtamd::ST_NODES0;
+		cnt.stage_node_visits[k] = static_cast<int64_t>(sum[b]);
+		cnt.stage_tri_tests[k] = static_cast<int64_t>(sum[b + 1]);
+		cnt.stage_candidates[k] = static_cast<int64_t>(sum[b + 2]);
+		cnt.stage_sphere_tests[k] = static_cast<int64_t>(sum[b + 3]);
+		cnt.node_visits += cnt.stage_node_visits[k];
+		cnt.tri_tests += cnt.stage_tri_tests[k];
+		cnt.candidates += cnt.stage_candidates[k];
+		cnt.sphere_tests += cnt.stage_sphere_tests[k];
+	}
+	cnt.trace_launches = cnt.stage_launches[0] + cnt.stage_launches[1] + cnt.stage_launches[2];
+	if (io && sum[rtamd::ST_MAX_BITS]) {
 		double m;
-		unsigned long long b = s->ctr_host->max_bits;
+		const unsigned long long b = sum[rtamd::ST_MAX_BITS];
 		std::memcpy(&m, &b, sizeof(m));
 		cnt.intersection_max = std::max(cnt.intersection_max, m);
 	}

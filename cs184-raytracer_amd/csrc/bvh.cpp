@@ -99,6 +99,43 @@ struct Builder {
 	}
 };
 
+// Padded world-space box of an object-space box (the eight corners through fwd).  Used
+// only to skip geometries a ray cannot hit; a degenerate transform disables it.
+void world_box(const Geometry& g, const double lo[3], const double hi[3], DGeom& d) {
+	bool finite = std::isfinite(g.det) && g.det != 0;
+	for (int i = 0; i < 3; i++)
+		for (int j = 0; j < 4; j++) finite = finite && std::isfinite(g.fwd.m[i][j]) && std::isfinite(g.inv.m[i][j]);
+	for (int k = 0; k < 3; k++) {
+		d.wlo[k] = -INFINITY;
+		d.whi[k] = INFINITY;
+	}
+	if (!finite) return;
+	if (!(lo[0] <= hi[0] && lo[1] <= hi[1] && lo[2] <= hi[2])) {  // empty mesh: nothing to hit
+		for (int k = 0; k < 3; k++) {
+			d.wlo[k] = INFINITY;
+			d.whi[k] = -INFINITY;
+		}
+		return;
+	}
+	double wl[3] = {INFINITY, INFINITY, INFINITY}, wh[3] = {-INFINITY, -INFINITY, -INFINITY};
+	double amax = 0;
+	for (int c = 0; c < 8; c++) {
+		const double p[4] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2], 1.0};
+		double w[4];
+		affine_apply(g.fwd, p, w);
+		for (int k = 0; k < 3; k++) {
+			wl[k] = std::min(wl[k], w[k]);
+			wh[k] = std::max(wh[k], w[k]);
+			amax = std::max(amax, std::fabs(w[k]));
+		}
+	}
+	const double pad = 1e-9 * amax + 1e-300;
+	for (int k = 0; k < 3; k++) {
+		d.wlo[k] = wl[k] - pad;
+		d.whi[k] = wh[k] + pad;
+	}
+}
+
 }  // namespace
 
 FlatScene flatten_scene(const Scene& s) {
@@ -146,6 +183,11 @@ FlatScene flatten_scene(const Scene& s) {
 			for (int k = 0; k < 3; k++) d.center[k] = g.center[k];
 			const float rr = g.radius * g.radius;  // fp32 product, geometry.cpp:53
 			d.rr = static_cast<double>(rr);
+			// the reference's test compares against rr in object space: box radius sqrt(rr)
+			const double rad = std::sqrt(static_cast<double>(rr)) * (1.0 + 1e-12);
+			const double lo[3] = {g.center[0] - rad, g.center[1] - rad, g.center[2] - rad};
+			const double hi[3] = {g.center[0] + rad, g.center[1] + rad, g.center[2] + rad};
+			world_box(g, lo, hi, d);
 			fs.geoms.push_back(d);
 			continue;
 		}
@@ -159,6 +201,16 @@ FlatScene flatten_scene(const Scene& s) {
 		}
 		d.face_begin = static_cast<int32_t>(fs.face_geo.size());
 		d.face_count = static_cast<int32_t>(g.face_count);
+		{
+			double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+			for (int64_t i = 0; i < g.face_count; i++)
+				for (int v = 0; v < 3; v++)
+					for (int k = 0; k < 3; k++) {
+						lo[k] = std::min(lo[k], s.faces[g.face_begin + i].p[v][k]);
+						hi[k] = std::max(hi[k], s.faces[g.face_begin + i].p[v][k]);
+					}
+			world_box(g, lo, hi, d);
+		}
 		auto emit = [&](int64_t local) {
 			const Face& f = s.faces[g.face_begin + local];
 			DFaceGeo fg{};
@@ -226,7 +278,7 @@ FlatScene flatten_scene(const Scene& s) {
 				bld.order.push_back(kv.second);
 			}
 			bld.build(0, static_cast<int>(g.face_count), 0);
-			if (bld.max_depth + 2 >= kStackDepth && attempt == 0) continue;  // too deep: median splits
+			if (bld.max_depth + 2 > kStackDepth && attempt == 0) continue;  // too deep: median splits
 			// inner-node indices are global (fs.nodes); leaf face indices are relative to the mesh
 			for (int32_t local : bld.leaf_order) emit(local);
 			fs.max_bvh_depth = std::max(fs.max_bvh_depth, bld.max_depth);

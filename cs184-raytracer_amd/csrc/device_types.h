@@ -19,7 +19,7 @@ enum : int32_t { DLIGHT_POINT = 0, DLIGHT_DIRECTIONAL = 1, DLIGHT_AMBIENT = 2 };
 
 constexpr int kLinearFaces = 8;   // meshes up to this size are scanned linearly (no BVH)
 constexpr int kLeafFaces = 4;     // faces per LBVH leaf
-constexpr int kStackDepth = 48;   // traversal stack entries per lane (LDS)
+constexpr int kStackDepth = 32;   // traversal stack entries per lane (LDS); LBVH depth <= 30
 
 struct alignas(16) DGeom {
 	double fwd[3][4];     // forwardTransform rows
@@ -27,6 +27,7 @@ struct alignas(16) DGeom {
 	double center[3];     // sphere centre (w == 1 implied)
 	double rr;            // (double)(radius_ * radius_) with the product in fp32 (geometry.cpp:53)
 	double bb_min[3], bb_max[3];   // Mesh bounding box (object space) for the gate
+	double wlo[3], whi[3];         // padded world-space box of the geometry (culling only)
 	int32_t kind;         // 0 sphere, 1 mesh
 	int32_t flip;         // transformDeterminant() < 0 (geometry.cpp:42-43)
 	int32_t gate;         // hitsBoundingBox gate active (geometry.cpp:72)

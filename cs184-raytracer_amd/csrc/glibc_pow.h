@@ -29,9 +29,11 @@ RT_HD uint32_t top12(double x) { return static_cast<uint32_t>(bits(x) >> 52); }
 constexpr uint64_t kOff = 0x3fe6955500000000ULL;
 constexpr uint32_t kSignBias = 0x800 << 7;
 
-// log(x) = hi + lo for the (normalised) bit pattern ix
-RT_HD double log_inline(uint64_t ix, double* tail) {
-	using namespace glibc_pow_data;
+// log(x) = hi + lo for the (normalised) bit pattern ix; kLogTab may live in LDS
+RT_HD double log_inline(uint64_t ix, double* tail, const double* kLogTab) {
+	using glibc_pow_data::kLn2hi;
+	using glibc_pow_data::kLn2lo;
+	using glibc_pow_data::kLogPoly;
 	const uint64_t tmp = ix - kOff;
 	const int i = static_cast<int>((tmp >> 45) % 128);
 	const int k = static_cast<int>(static_cast<int64_t>(tmp) >> 52);
@@ -85,8 +87,12 @@ RT_HD double specialcase(double tmp, uint64_t sbits, uint64_t ki) {
 	return y * 0x1p-1022;
 }
 
-RT_HD double exp_inline(double x, double xtail, uint32_t sign_bias) {
-	using namespace glibc_pow_data;
+RT_HD double exp_inline(double x, double xtail, uint32_t sign_bias, const uint64_t* kExpTab) {
+	using glibc_pow_data::kExpPoly;
+	using glibc_pow_data::kInvLn2N;
+	using glibc_pow_data::kNegLn2hiN;
+	using glibc_pow_data::kNegLn2loN;
+	using glibc_pow_data::kShift;
 	uint32_t abstop = top12(x) & 0x7ff;
 	if (abstop - 0x3c9 >= 0x408 - 0x3c9) {  // |x| < 2^-54 or |x| >= 512
 		if (static_cast<int32_t>(abstop - 0x3c9) < 0) {
@@ -134,7 +140,9 @@ RT_HD bool issignaling(double x) {
 
 }  // namespace glibc_pow_detail
 
-RT_HD double glibc_pow(double x, double y) {
+// logtab/exptab: glibc_pow_data::kLogTab / kExpTab or copies of them (e.g. in LDS)
+RT_HD double glibc_pow(double x, double y, const double* logtab = glibc_pow_data::kLogTab,
+                       const uint64_t* exptab = glibc_pow_data::kExpTab) {
 	using namespace glibc_pow_detail;
 	uint32_t sign_bias = 0;
 	uint64_t ix = bits(x), iy = bits(y);
@@ -176,10 +184,10 @@ RT_HD double glibc_pow(double x, double y) {
 		}
 	}
 	double lo;
-	const double hi = log_inline(ix, &lo);
+	const double hi = log_inline(ix, &lo, logtab);
 	const double ehi = y * hi;
 	const double elo = fma_(y, lo, fma_(hi, y, -ehi));
-	return exp_inline(ehi, elo, sign_bias);
+	return exp_inline(ehi, elo, sign_bias, exptab);
 }
 
 }  // namespace rtamd

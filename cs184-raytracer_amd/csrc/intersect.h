@@ -1,0 +1,566 @@
+// Device-side intersection code of the hot path (included by trace.hip only).
+//
+// Numerics: binary64, -ffp-contract=off, every expression in the reference's Eigen 3.2.2
+// evaluation order:
+//   Vector4d dot   (a0 b0 + a2 b2) + (a1 b1 + a3 b3); for directions/normals the w products
+//                  are exact zeros and are dropped (dot4z, sq4)
+//   Vector3d norm  a0^2 + (a1^2 + a2^2)
+//   T * v          rows sequential ((m0 v0 + m1 v1) + m2 v2) + m3 v3
+//   invT * n       (M0k n0 + M2k n2) + (M1k n1 + M3k n3)
+//   normalized()   division by the norm; normalize() multiplies by the reciprocal
+//
+// Acceleration (new design, exact): LBVH per mesh, world-space boxes per geometry, and
+// conservative pre-tests that only ever skip work whose outcome is already decided.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include "device_types.h"
+#include "trace.h"
+
+namespace rtamd {
+namespace dev {
+
+constexpr int kBlock = 128;  // 2 waves; LDS traversal stack = kStackDepth x kBlock x 4 B
+
+// Scene data read at a wave-uniform address goes through the constant address space so
+// it is fetched with scalar (SMEM) loads into SGPRs: one fetch per wave, no VGPRs.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* uniform_ptr(const T* p) {
+	return (const __attribute__((address_space(4))) T*)(p);
+}
+template <bool kUniform, typename T>
+__device__ __forceinline__ auto scene_ptr(const T* p) {
+	if constexpr (kUniform)
+		return uniform_ptr(p);
+	else
+		return p;
+}
+
+struct V3 {
+	double x, y, z;
+};
+__device__ __forceinline__ V3 mk(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator-(V3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 operator*(double s, V3 a) { return mk(s * a.x, s * a.y, s * a.z); }
+template <typename P>
+__device__ __forceinline__ V3 load3(P p) { return mk(p[0], p[1], p[2]); }
+
+// Vector4d::dot of two vectors whose w is (+-)0: the w term contributes an exact zero
+__device__ __forceinline__ double dot4z(V3 a, V3 b) { return (a.x * b.x + a.z * b.z) + a.y * b.y; }
+// Vector4d::squaredNorm with w == 0: exact (y^2 + 0 == y^2)
+__device__ __forceinline__ double sq4(V3 a) { return (a.x * a.x + a.z * a.z) + a.y * a.y; }
+// isZero(): all |c| <= 1e-12 (w is zero)
+__device__ __forceinline__ bool is_zero3(V3 a) { return fabs(a.x) <= 1e-12 && fabs(a.y) <= 1e-12 && fabs(a.z) <= 1e-12; }
+__device__ __forceinline__ V3 div3(V3 a, double n) { return mk(a.x / n, a.y / n, a.z / n); }
+
+template <typename M>
+__device__ __forceinline__ V3 xf_point(M m, V3 p) {
+	return mk(((m[0][0] * p.x + m[0][1] * p.y) + m[0][2] * p.z) + m[0][3],
+	          ((m[1][0] * p.x + m[1][1] * p.y) + m[1][2] * p.z) + m[1][3],
+	          ((m[2][0] * p.x + m[2][1] * p.y) + m[2][2] * p.z) + m[2][3]);
+}
+template <typename M>
+__device__ __forceinline__ V3 xf_dir(M m, V3 d) {
+	return mk((m[0][0] * d.x + m[0][1] * d.y) + m[0][2] * d.z, (m[1][0] * d.x + m[1][1] * d.y) + m[1][2] * d.z,
+	          (m[2][0] * d.x + m[2][1] * d.y) + m[2][2] * d.z);
+}
+// inverseTransform().matrix().transpose() * n (geometry.cpp:40)
+template <typename M>
+__device__ __forceinline__ V3 xf_normal(M m, V3 n) {
+	return mk((m[0][0] * n.x + m[2][0] * n.z) + m[1][0] * n.y, (m[0][1] * n.x + m[2][1] * n.z) + m[1][1] * n.y,
+	          (m[0][2] * n.x + m[2][2] * n.z) + m[1][2] * n.y);
+}
+
+__device__ __forceinline__ void raise_error(DeviceCounters* c, int code) { atomicCAS(&c->error, 0, code); }
+
+// Ray::direction(dir) (rtbase.h:17-23): reject |c| <= 1e-12, then dir.normalized()
+__device__ __forceinline__ V3 ray_dir(V3 d, DeviceCounters* c) {
+	if (is_zero3(d)) raise_error(c, DERR_NO_DIRECTION);
+	return div3(d, sqrt(sq4(d)));
+}
+
+// Matrix3d::determinant of the matrix with columns c0, c1, c2 (LU/Determinant.h:61-69)
+__device__ __forceinline__ double det3(V3 c0, V3 c1, V3 c2) {
+	return (c0.x * (c1.y * c2.z - c2.y * c1.z) - c1.x * (c0.y * c2.z - c2.y * c0.z)) + c2.x * (c0.y * c1.z - c1.y * c0.z);
+}
+
+// hitsBoundingBox, verbatim (geometry.cpp:5-29)
+template <typename P>
+__device__ bool hits_bounding_box(V3 o, V3 d, P mn, P mx) {
+	const double oa[3] = {o.x, o.y, o.z}, da[3] = {d.x, d.y, d.z};
+#pragma unroll
+	for (int axis = 0; axis < 3; axis++) {
+#pragma unroll
+		for (int bn = 0; bn < 2; bn++) {
+			const double mag = da[axis];
+			if (mag == 0.0) continue;
+			const double t = ((bn ? mx : mn)[axis] - oa[axis]) / mag;
+			if (t < 0) continue;
+			bool inside = true;
+#pragma unroll
+			for (int a2 = 0; a2 < 3; a2++) {
+				if (a2 == axis) continue;
+				const double p = oa[a2] + t * da[a2];
+				if (p < mn[a2] || p > mx[a2]) inside = false;
+			}
+			if (inside) return true;
+		}
+	}
+	return false;
+}
+
+// Per-lane work counters (algorithmic bytes/flops of the roofline)
+struct WorkStats {
+	uint32_t nodes, tris, cands, spheres;
+};
+
+struct MeshBest {
+	double dist;
+	int32_t face;   // global face index, -1 = none
+	int32_t id;     // reference order within the mesh (tie-break)
+	double a, b;
+	V3 n;
+};
+
+// Exact pre-tests on q = num / den (den != 0): true only when the correctly rounded
+// quotient certainly satisfies the predicate, so skipping the division cannot change a
+// decision.  2^-1000 keeps clear of an underflow of the quotient to -0.
+__device__ __forceinline__ bool quotient_surely_negative(double num, double den) {
+	return ((num < 0) != (den < 0)) && fabs(num) > fabs(den) * 0x1p-1000;
+}
+// |num| > |den| * lim * 1.001 (same signs) implies fl(num / den) > lim; the threshold must
+// be a normal number so that its own rounding stays below the 0.1% slack (lim >= 2^-900).
+__device__ __forceinline__ bool quotient_surely_above(double num, double den, double lim) {
+	const double thr = fabs(den) * (lim * 1.001);
+	return ((num < 0) == (den < 0)) && thr >= 0x1p-1000 && fabs(num) > thr;
+}
+
+// One iteration of the face loop of geometry.cpp:78-124.  Accepts the face when it is
+// strictly closer, or equally close with a smaller reference index: over any visiting
+// order this selects the same face as the reference's in-order scan.
+// Returns true when kAnyHit and the face passes (the caller's question is answered).
+template <bool kAnyHit, bool kUniform = false>
+__device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn, bool reverse,
+                                          double any_limit, MeshBest& best, WorkStats& ws) {
+	ws.tris++;
+	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
+	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	const V3 rhs = o - p0;
+	const double D = det3(va, vb, nd);
+	if (D == 0) return false;
+	const double Da = det3(rhs, vb, nd);
+	if (quotient_surely_negative(Da, D) || quotient_surely_above(Da, D, 1.0)) return false;
+	const double a = Da / D;
+	if (a < 0 || a > 1) return false;
+	const double Db = det3(va, rhs, nd);
+	if (quotient_surely_negative(Db, D) || quotient_surely_above(Db, D, 1.0)) return false;
+	const double b = Db / D;
+	if (b < 0 || a + b > 1) return false;
+	const double Dt = det3(va, vb, rhs);
+	if (quotient_surely_negative(Dt, D)) return false;
+	// dist = t * dn with dn = |d|_3 within a few ulps of 1: t > 1.001 * best * 1.001 cannot win
+	if (best.dist < INFINITY && best.dist >= 0x1p-900 && quotient_surely_above(Dt, D, best.dist * 1.001)) return false;
+	const double t = Dt / D;
+	if (t < 0) return false;
+	const double dist = t * dn;
+	const int32_t id = scene_ptr<kUniform>(S.fid)[f];
+	if (!(dist < best.dist || (dist == best.dist && id < best.id))) return false;
+	ws.cands++;
+	const auto N = scene_ptr<kUniform>(S.fnrm) + f;
+	const double w0 = (1.0 - a) - b;
+	const V3 n0 = load3(N->n0), n1 = load3(N->n1), n2 = load3(N->n2);
+	const V3 tn = mk((w0 * n0.x + a * n1.x) + b * n2.x, (w0 * n0.y + a * n1.y) + b * n2.y, (w0 * n0.z + a * n1.z) + b * n2.z);
+	const bool front = dot4z(tn, d) < 0;
+	if (!front ^ reverse) return false;
+	best.dist = dist;
+	best.face = f;
+	best.id = id;
+	best.a = a;
+	best.b = b;
+	best.n = tn;
+	return kAnyHit && dist < any_limit;
+}
+
+// Slab test of a padded box; conservative: the interval is widened by a relative 1e-9.
+template <typename P>
+__device__ __forceinline__ bool slab(P lo, P hi, V3 o, V3 inv, double tlimit, double& tnear) {
+	const double tx0 = (lo[0] - o.x) * inv.x, tx1 = (hi[0] - o.x) * inv.x;
+	const double ty0 = (lo[1] - o.y) * inv.y, ty1 = (hi[1] - o.y) * inv.y;
+	const double tz0 = (lo[2] - o.z) * inv.z, tz1 = (hi[2] - o.z) * inv.z;
+	double tmin = fmax(fmax(fmin(tx0, tx1), fmin(ty0, ty1)), fmin(tz0, tz1));
+	double tmax = fmin(fmin(fmax(tx0, tx1), fmax(ty0, ty1)), fmax(tz0, tz1));
+	tmin -= 1e-9 * fabs(tmin);
+	tmax += 1e-9 * fabs(tmax);
+	tnear = tmin;
+	return tmax >= tmin && tmax >= 0.0 && tmin <= tlimit;
+}
+
+__device__ __forceinline__ V3 safe_inv(V3 d) {
+	return mk(1.0 / (d.x != 0.0 ? d.x : copysign(1e-300, d.x)), 1.0 / (d.y != 0.0 ? d.y : copysign(1e-300, d.y)),
+	          1.0 / (d.z != 0.0 ? d.z : copysign(1e-300, d.z)));
+}
+
+__device__ __forceinline__ double prune_limit(double best_dist) { return best_dist * (1.0 + 4e-9); }
+
+// Mesh::calculateIntNormInObjSpace (geometry.cpp:69-126) with an LBVH in place of the
+// linear scan for large meshes.
+//   kAnyHit = false: the reference's closest face (returns found, Po, No).
+//   kAnyHit = true: shadow query; returns true as soon as a passing face has
+//   dist < any_limit (the caller knows that settles occlusion); nodes beyond
+//   prune_cap are skipped (faces there cannot decide it either).  Otherwise completes
+//   like the closest-hit search restricted to dist <= prune_cap.
+template <bool kAnyHit, typename GP>
+__device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
+                         double prune_cap, V3& Po, V3& No, bool& settled, double& found_dist, int32_t* stack,
+                         DeviceCounters* ctr, WorkStats& ws) {
+	settled = false;
+	if (G->gate && !hits_bounding_box(o, d, G->bb_min, G->bb_max)) return false;
+	const double dn = sqrt(d.x * d.x + (d.y * d.y + d.z * d.z));  // Vector3d::norm
+	const V3 nd = -d;
+	MeshBest best;
+	best.dist = INFINITY;
+	best.face = -1;
+	best.id = 0x7fffffff;
+	if (G->bvh_root < 0) {
+		for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++)
+			if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+				settled = true;
+				return true;
+			}
+	} else {
+		const V3 inv = safe_inv(d);
+		int32_t node = G->bvh_root;
+		int sp = 0;
+		for (;;) {
+			ws.nodes++;
+			const DBvhNode* N = S.nodes + node;
+			double tn0, tn1;
+			const double lim = fmin(prune_limit(best.dist), prune_cap);
+			const bool h0 = slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
+			const bool h1 = slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+			const int first = (h0 && h1 && tn1 < tn0) ? 1 : 0;
+			int32_t next = -1;
+#pragma unroll
+			for (int k = 0; k < 2; k++) {
+				const int c = first ^ k;
+				if (!(c ? h1 : h0)) continue;
+				if (k == 1 && (c ? tn1 : tn0) > fmin(prune_limit(best.dist), prune_cap)) continue;
+				const int32_t cf = N->first[c], cc = N->count[c];
+				if (cc > 0) {
+					const int32_t f0 = G->face_begin + cf;
+					for (int32_t f = f0; f < f0 + cc; f++)
+						if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+							settled = true;
+							return true;
+						}
+				} else if (next < 0) {
+					next = cf;
+				} else if (sp < kStackDepth) {
+					stack[sp++ * kBlock] = cf;
+				} else {
+					raise_error(ctr, DERR_STACK);
+				}
+			}
+			if (next < 0) {
+				if (sp == 0) break;
+				next = stack[--sp * kBlock];
+			}
+			node = next;
+		}
+	}
+	found_dist = best.dist;
+	if (best.face < 0) return false;
+	const DFaceGeo* F = S.fgeo + best.face;
+	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	// face.points_[0] + vec4dFrom3d(a * va + b * vb)
+	Po = mk(p0.x + (best.a * va.x + best.b * vb.x), p0.y + (best.a * va.y + best.b * vb.y),
+	        p0.z + (best.a * va.z + best.b * vb.z));
+	No = best.n;
+	return true;
+}
+
+// Sphere::calculateIntNormInObjSpace (geometry.cpp:47-67)
+template <typename GP>
+__device__ __forceinline__ bool sphere_hit(GP G, V3 o, V3 d, bool reverse, V3& Po, V3& No) {
+	const V3 c = load3(G->center);
+	const V3 oc = o - c;
+	const double a = sq4(d);
+	const double b = 2 * dot4z(d, oc);
+	const double cc = sq4(oc) - G->rr;
+	const double disc = b * b - (4 * a) * cc;
+	if (disc < 0) return false;
+	const double t = reverse ? (-b + sqrt(disc)) / (2 * a) : (-b - sqrt(disc)) / (2 * a);
+	if (t < 0) return false;
+	Po = o + t * d;
+	No = Po - c;
+	return true;
+}
+
+// Closest hit of Scene::castRay (scene.cpp:142-167): world distance, strict `<` in
+// insertion order.  A geometry whose padded world box the ray misses, or enters beyond
+// the current best distance, cannot be the answer and is skipped without its
+// object-space transform.
+__device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, double& best_dist, int& best_geom, V3& hitP,
+                            V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WorkStats& ws) {
+	bool found = false;
+	const V3 winv = safe_inv(d);
+	for (int g = 0; g < S.n_geoms; g++) {
+		const auto G = uniform_ptr(S.geoms) + g;
+		double tw;
+		if (!slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw)) continue;
+		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
+		const V3 oo = xf_point(G->inv, o);
+		const V3 dd = ray_dir(xf_dir(G->inv, d), ctr);
+		V3 Po, No;
+		bool hit, settled;
+		double fd;
+		if (G->kind == DGEOM_SPHERE) {
+			ws.spheres++;
+			hit = sphere_hit(G, oo, dd, reverse, Po, No);
+		} else {
+			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, Po, No, settled, fd, stack, ctr, ws);
+		}
+		if (!hit) continue;
+		const V3 Pw = xf_point(G->fwd, Po);
+		const double dist = sqrt(sq4(Pw - o));
+		if (found && dist >= best_dist) continue;
+		found = true;
+		best_dist = dist;
+		best_geom = g;
+		hitP = Pw;
+		hitNobj = No;
+	}
+	return found;
+}
+
+// Shadow test of scene.cpp:90-93: castRay(...) && distToOccluder <= distToLight, i.e.
+// some geometry's hit (its reference-chosen face) lies within dist_light.  Meshes first
+// try an any-hit search that decides the common cases exactly: a face with object-space
+// t well inside the light distance occludes (the closest face is nearer still), and no
+// face up to slightly beyond it means no occlusion.  Only a closest face within a
+// relative 1e-7 of the light distance falls back to the reference's full comparison.
+__device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, int32_t* stack,
+                         DeviceCounters* ctr, WorkStats& ws) {
+	const V3 winv = safe_inv(d);
+	const bool inf_light = dist_light == INFINITY;
+	for (int g = 0; g < S.n_geoms; g++) {
+		const auto G = uniform_ptr(S.geoms) + g;
+		double tw;
+		if (!slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw)) continue;
+		const V3 oo = xf_point(G->inv, o);
+		const V3 draw = xf_dir(G->inv, d);
+		if (is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
+		const double nrm = sqrt(sq4(draw));  // object-space length of the unit world direction
+		const V3 dd = div3(draw, nrm);
+		V3 Po, No;
+		bool hit, settled = false;
+		double fd;
+		if (G->kind == DGEOM_SPHERE) {
+			ws.spheres++;
+			hit = sphere_hit(G, oo, dd, reverse, Po, No);
+		} else if (inf_light) {
+			hit = mesh_hit<true>(S, G, oo, dd, reverse, INFINITY, INFINITY, Po, No, settled, fd, stack, ctr, ws);
+		} else {
+			// world distance of object-space dist t is ~ t / nrm
+			const double tl = dist_light * nrm;
+			const double cap = tl * (1.0 + 1e-7) + 1e-300;
+			hit = mesh_hit<true>(S, G, oo, dd, reverse, tl * (1.0 - 1e-7), cap, Po, No, settled, fd, stack, ctr, ws);
+			// No face up to `cap` was missed by the capped search, so a closest face beyond
+			// it lies beyond the light.  A closest face inside the 1e-7 band is decided
+			// exactly from the reference's own face choice (full closest-face search).
+			if (hit && !settled) {
+				if (fd > cap) continue;
+				hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, Po, No, settled, fd, stack, ctr, ws);
+			}
+		}
+		if (!hit) continue;
+		if (inf_light || settled) return true;
+		const V3 Pw = xf_point(G->fwd, Po);
+		if (sqrt(sq4(Pw - o)) <= dist_light) return true;
+	}
+	return false;
+}
+
+
+// ---------------------------------------------------------------- wave-packet traversal
+// For coherent rays (8x8 primary-ray tiles, shadow rays of such a tile towards one light)
+// all 64 lanes of a wave traverse together: the wave visits the union of the nodes its
+// lanes need, in one wave-uniform order (majority near-first), so node and face records
+// are scalar loads (SGPRs) and the lanes never diverge on control flow.  Per-lane results
+// are identical to the per-lane traversal: every lane still tests every face it would
+// test there (pruning and tie-breaks are per lane), it may only test a few more.
+// Callers must reach these functions with all lanes (inactive lanes pass on = false).
+
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
+
+template <bool kAnyHit, typename GP>
+__device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, bool on, double any_limit,
+                                double prune_cap, V3& Po, V3& No, bool& settled, double& found_dist,
+                                int32_t* wstack, WorkStats& ws) {
+	settled = false;
+	if (G->gate) on = on && hits_bounding_box(o, d, G->bb_min, G->bb_max);
+	const double dn = sqrt(d.x * d.x + (d.y * d.y + d.z * d.z));  // Vector3d::norm
+	const V3 nd = -d;
+	MeshBest best;
+	best.dist = INFINITY;
+	best.face = -1;
+	best.id = 0x7fffffff;
+	bool live = on;
+	if (wave_any(live)) {
+		if (G->bvh_root < 0) {
+			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++)
+				if (live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+					settled = true;
+					live = false;
+				}
+		} else {
+			const V3 inv = safe_inv(d);
+			const auto nodes = uniform_ptr(S.nodes);
+			int32_t node = G->bvh_root;
+			int sp = 0;
+			for (;;) {
+				const auto N = nodes + node;
+				if (live) ws.nodes++;
+				double tn0 = 0, tn1 = 0;
+				const double lim = fmin(prune_limit(best.dist), prune_cap);
+				const bool h0 = live && slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
+				const bool h1 = live && slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
+				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
+				const int first = (2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0;
+				int32_t next = -1;
+#pragma unroll
+				for (int k = 0; k < 2; k++) {
+					const int c = first ^ k;
+					bool want = c ? h1 : h0;
+					if (k == 1) want = want && live && (c ? tn1 : tn0) <= fmin(prune_limit(best.dist), prune_cap);
+					if (!wave_any(want)) continue;
+					const int32_t cf = N->first[c], cc = N->count[c];
+					if (cc > 0) {
+						const int32_t f0 = G->face_begin + cf;
+						for (int32_t f = f0; f < f0 + cc; f++)
+							if (want && live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+								settled = true;
+								live = false;
+							}
+					} else if (next < 0) {
+						next = cf;
+					} else if (sp < kStackDepth) {
+						wstack[sp++] = cf;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
+					}
+				}
+				if (!wave_any(live)) break;
+				if (next < 0) {
+					if (sp == 0) break;
+					next = wstack[--sp];
+				}
+				node = next;
+			}
+		}
+	}
+	found_dist = best.dist;
+	if (!on || best.face < 0) return false;
+	const DFaceGeo* F = S.fgeo + best.face;
+	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	Po = mk(p0.x + (best.a * va.x + best.b * vb.x), p0.y + (best.a * va.y + best.b * vb.y),
+	        p0.z + (best.a * va.z + best.b * vb.z));
+	No = best.n;
+	return true;
+}
+
+__device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, bool on, double& best_dist,
+                                   int& best_geom, V3& hitP, V3& hitNobj, int32_t* wstack, DeviceCounters* ctr,
+                                   WorkStats& ws) {
+	bool found = false;
+	const V3 winv = safe_inv(d);
+	for (int g = 0; g < S.n_geoms; g++) {
+		const auto G = uniform_ptr(S.geoms) + g;
+		double tw;
+		const bool cand = on && slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw);
+		if (!wave_any(cand)) continue;
+		const V3 oo = xf_point(G->inv, o);
+		const V3 draw = xf_dir(G->inv, d);
+		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
+		const V3 dd = div3(draw, sqrt(sq4(draw)));
+		V3 Po = mk(0, 0, 0), No = mk(0, 0, 0);
+		bool hit, settled;
+		double fd;
+		if (G->kind == DGEOM_SPHERE) {
+			if (cand) ws.spheres++;
+			hit = cand && sphere_hit(G, oo, dd, reverse, Po, No);
+		} else {
+			hit = mesh_hit_packet<false>(S, G, oo, dd, reverse, cand, INFINITY, INFINITY, Po, No, settled, fd, wstack, ws);
+		}
+		if (hit) {
+			const V3 Pw = xf_point(G->fwd, Po);
+			const double dist = sqrt(sq4(Pw - o));
+			if (!(found && dist >= best_dist)) {
+				found = true;
+				best_dist = dist;
+				best_geom = g;
+				hitP = Pw;
+				hitNobj = No;
+			}
+		}
+	}
+	return found;
+}
+
+// Packet form of occluded(): same decisions per lane (see occluded()).
+__device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, bool on,
+                                int32_t* wstack, DeviceCounters* ctr, WorkStats& ws) {
+	const V3 winv = safe_inv(d);
+	const bool inf_light = dist_light == INFINITY;
+	bool occ = false;
+	for (int g = 0; g < S.n_geoms; g++) {
+		const auto G = uniform_ptr(S.geoms) + g;
+		double tw;
+		const bool cand = on && !occ && slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);
+		if (!wave_any(cand)) continue;
+		const V3 oo = xf_point(G->inv, o);
+		const V3 draw = xf_dir(G->inv, d);
+		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
+		const double nrm = sqrt(sq4(draw));
+		const V3 dd = div3(draw, nrm);
+		V3 Po = mk(0, 0, 0), No = mk(0, 0, 0);
+		bool hit, settled = false;
+		double fd = INFINITY;
+		if (G->kind == DGEOM_SPHERE) {
+			if (cand) ws.spheres++;
+			hit = cand && sphere_hit(G, oo, dd, reverse, Po, No);
+		} else {
+			const double tl = inf_light ? INFINITY : dist_light * nrm;
+			const double cap = inf_light ? INFINITY : tl * (1.0 + 1e-7) + 1e-300;
+			hit = mesh_hit_packet<true>(S, G, oo, dd, reverse, cand, inf_light ? INFINITY : tl * (1.0 - 1e-7), cap, Po,
+			                            No, settled, fd, wstack, ws);
+			// closest face inside the 1e-7 band around the light: the reference's exact choice
+			const bool band = cand && hit && !settled && !inf_light && fd <= cap;
+			if (cand && hit && !settled && !inf_light && fd > cap) hit = false;
+			if (wave_any(band)) {
+				bool s2;
+				double fd2;
+				V3 P2 = mk(0, 0, 0), N2 = mk(0, 0, 0);
+				const bool h2 = mesh_hit_packet<false>(S, G, oo, dd, reverse, band, INFINITY, INFINITY, P2, N2, s2, fd2,
+				                                       wstack, ws);
+				if (band) {
+					hit = h2;
+					Po = P2;
+				}
+			}
+		}
+		if (cand && hit) {
+			if (inf_light || settled) {
+				occ = true;
+			} else {
+				const V3 Pw = xf_point(G->fwd, Po);
+				if (sqrt(sq4(Pw - o)) <= dist_light) occ = true;
+			}
+		}
+	}
+	return occ;
+}
+
+}  // namespace dev
+}  // namespace rtamd

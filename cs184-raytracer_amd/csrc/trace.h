@@ -6,6 +6,8 @@
 
 namespace rtamd {
 
+constexpr int kMaxShadowLights = 64;
+
 struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DGeom* geoms;
 	const DMaterial* mats;
@@ -16,7 +18,8 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DBvhNode* nodes;
 	DCamera cam;
 	int32_t n_geoms, n_lights, n_nonambient;
-	int32_t pad;
+	int32_t occl_stride;                      // bytes per ray in RayLevel::occl (n_nonambient rounded to 8)
+	int32_t shadow_light[kMaxShadowLights];  // j-th non-ambient light -> light index
 };
 
 // One wavefront level of ray records (structure of arrays).
@@ -24,6 +27,12 @@ struct RayLevel {
 	// ray in (unused at level 0: primary rays are generated from the pixel index)
 	double *ox, *oy, *oz, *dx, *dy, *dz;
 	uint8_t* inside;
+	// closest hit (k_closest -> k_shadow, k_shade)
+	int32_t* hgeom;              // hit geometry, -1 = miss
+	double *hpx, *hpy, *hpz;     // world hit point
+	double *hnx, *hny, *hnz;     // shading normal (flipped if inside, normalised)
+	int32_t* hit_list;           // indices of rays that hit (order of discovery)
+	uint8_t* occl;               // [ray][non-ambient light] shadow verdicts
 	// node out
 	double *cr, *cg, *cb;        // local colour, overwritten with the final colour by reduce
 	double *kr, *kg, *kb;        // reflective weight (after TIR), valid when child_refl >= 0
@@ -38,23 +47,39 @@ struct FrameGeometry {
 	int32_t intersection_only;
 };
 
-// Device counters: first error code, next-level ray count, shaded hits (x non-ambient
-// lights = shadow rays), running max (bits) for --intersection-only, children spawned
+// Device counters: first error code, next-level ray count, hits of the level being
+// traced (k_closest -> k_shadow), shaded hits (x non-ambient lights = shadow rays),
+// running max (bits) for --intersection-only, children spawned and work counters.
 struct DeviceCounters {
 	int32_t error;
 	int32_t next_count;
-	unsigned long long hits;
-	unsigned long long max_bits;
-	unsigned long long refl, refr;
-	unsigned long long node_visits, tri_tests, candidates, sphere_tests;
+	int32_t level_hits;
+	int32_t pad;
 };
 
-hipError_t launch_trace_level(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n,
-                              int remaining_depth, const RayLevel& cur, const RayLevel& next,
-                              DeviceCounters* ctr, hipStream_t stream);
+// Statistics are sharded: a single word takes only ~88 atomics/us on MI355X
+// (MI355X_MICROARCH.md, "dequeue"), so every block adds into shard blockIdx % kStatShards
+// (one 128-B line each) and the host sums the shards.
+constexpr int kStatShards = 256;
+enum StatSlot : int {
+	ST_HITS = 0, ST_REFL, ST_REFR, ST_MAX_BITS,
+	ST_NODES0, ST_TRIS0, ST_CANDS0, ST_SPHERES0,   // k_closest
+	ST_NODES1, ST_TRIS1, ST_CANDS1, ST_SPHERES1,   // k_shadow
+	ST_COUNT
+};
+constexpr int kStatStride = 16;  // u64 per shard (128 B)
+
+// One wavefront level: closest hit, shadow rays, shading + children.  ev[0..3] (may be
+// null) are recorded on `stream` before k_closest and after each of the three kernels;
+// launches[k] counts the launches of kernel k.
+// packet_mask selects wave-packet traversal per kernel and level class
+enum : int { kPacketClosest0 = 1, kPacketClosestN = 2, kPacketShadow0 = 4, kPacketShadowN = 8 };
+hipError_t launch_level(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
+                        const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
+                        hipStream_t stream, hipEvent_t* ev, int* launches, int packet_mask);
 hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream);
 hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8_t* out_rgb8,
-                         int32_t intersection_only, DeviceCounters* ctr, hipStream_t stream);
+                         int32_t intersection_only, unsigned long long* stats, hipStream_t stream);
 hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uint8_t* out_rgb8, hipStream_t stream);
 hipError_t launch_selftest_math(int op, const double* x, const double* y, double* out, int64_t n, hipStream_t stream);
 

@@ -62,7 +62,10 @@ class rt_counters(ctypes.Structure):
                 ("refract_rays", ctypes.c_int64), ("pixels", ctypes.c_int64), ("intersection_max", ctypes.c_double),
                 ("kernel_ms", ctypes.c_double), ("levels", ctypes.c_int32), ("trace_launches", ctypes.c_int32),
                 ("node_visits", ctypes.c_int64), ("tri_tests", ctypes.c_int64), ("candidates", ctypes.c_int64),
-                ("sphere_tests", ctypes.c_int64)]
+                ("sphere_tests", ctypes.c_int64), ("stage_ms", ctypes.c_double * 3),
+                ("stage_launches", ctypes.c_int32 * 3), ("stage_node_visits", ctypes.c_int64 * 2),
+                ("stage_tri_tests", ctypes.c_int64 * 2), ("stage_candidates", ctypes.c_int64 * 2),
+                ("stage_sphere_tests", ctypes.c_int64 * 2)]
 
 
 class rt_scene_info(ctypes.Structure):
@@ -158,6 +161,12 @@ class RenderStats:
     tri_tests: int
     candidates: int
     sphere_tests: int
+    stage_ms: tuple = ()            # (k_closest, k_shadow, k_shade) device ms
+    stage_launches: tuple = ()
+    stage_node_visits: tuple = ()   # (closest, shadow)
+    stage_tri_tests: tuple = ()
+    stage_candidates: tuple = ()
+    stage_sphere_tests: tuple = ()
 
     @property
     def rays(self) -> int:
@@ -168,7 +177,8 @@ class RenderStats:
 def _stats(c: rt_counters) -> RenderStats:
     return RenderStats(c.trace_rays, c.shadow_rays, c.reflect_rays, c.refract_rays, c.pixels, c.intersection_max,
                        c.kernel_ms, c.levels, c.trace_launches, c.node_visits, c.tri_tests, c.candidates,
-                       c.sphere_tests)
+                       c.sphere_tests, tuple(c.stage_ms), tuple(c.stage_launches), tuple(c.stage_node_visits),
+                       tuple(c.stage_tri_tests), tuple(c.stage_candidates), tuple(c.stage_sphere_tests))
 
 
 class Scene:

@@ -89,14 +89,18 @@ typedef struct rt_counters {
 	int64_t pixels;
 	double  intersection_max;   /* max over rendered pixels of maxCoeff (scene.cpp:50-53),
 	                               only with intersection_only                          */
-	double  kernel_ms;          /* summed device time of the trace kernels (HIP events) */
+	double  kernel_ms;          /* device time of the per-level kernels (HIP events)     */
 	int32_t levels;             /* wavefront levels executed (max over chunks)          */
-	int32_t trace_launches;     /* trace-kernel launches (levels summed over chunks)    */
-	/* work done by the trace kernels (algorithmic bytes/flops) */
+	int32_t trace_launches;     /* per-level kernel launches                             */
+	/* work done by the traversal kernels (algorithmic bytes/flops) */
 	int64_t node_visits;        /* LBVH nodes visited (2 child boxes tested each)       */
 	int64_t tri_tests;          /* ray-triangle (Cramer) tests                          */
 	int64_t candidates;         /* tests that reached the normal fetch + facing test    */
 	int64_t sphere_tests;       /* ray-sphere tests                                     */
+	/* per-kernel split: [0] k_closest (camera/secondary rays), [1] k_shadow, [2] k_shade */
+	double  stage_ms[3];
+	int32_t stage_launches[3];
+	int64_t stage_node_visits[2], stage_tri_tests[2], stage_candidates[2], stage_sphere_tests[2];
 } rt_counters;
 
 /* Scene::renderScene into a caller-owned host buffer of n_rows*W*3 doubles

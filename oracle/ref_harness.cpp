@@ -68,16 +68,27 @@ int main(int argc, char* argv[]) {
 	} else {
 		const int workers = std::max(1, programOptions.renderThreadsCount_);
 		const long block = 2000;  // scene.cpp:13
+		// RT_REF_ROWS=begin:end:step renders only those rows (bench.py's bounded CPU
+		// sample); the selected pixels are dealt in 2000-pixel blocks as above.
+		long rb = 0, re = rows, rs = 1;
+		if (const char* sel = std::getenv("RT_REF_ROWS")) {
+			if (std::sscanf(sel, "%ld:%ld:%ld", &rb, &re, &rs) != 3 || rb < 0 || re > rows || rs <= 0) {
+				std::fprintf(stderr, "refharness: bad RT_REF_ROWS\n");
+				return 1;
+			}
+		}
+		const long selected = (re > rb) ? ((re - rb + rs - 1) / rs) * cols : 0;
 		for (int w = 0; w < workers; w++) {
 			pid_t pid = fork();
 			if (pid < 0) { std::perror("fork"); return 1; }
 			if (pid == 0) {
 				Camera cam = scene.camera();
-				for (long start = (long)w * block; start < total; start += (long)workers * block) {
-					long end = std::min(start + block, total);
-					for (long i = start; i < end; i++) {
-						int r = (int)(i / cols);
-						int c = (int)(i % cols);
+				for (long start = (long)w * block; start < selected; start += (long)workers * block) {
+					long end = std::min(start + block, selected);
+					for (long k = start; k < end; k++) {
+						int r = (int)(rb + (k / cols) * rs);
+						int c = (int)(k % cols);
+						long i = (long)r * cols + c;
 						double rowFrac = (r + 0.5) / rows;  // scene.cpp:28
 						double colFrac = (c + 0.5) / cols;  // scene.cpp:29
 						Ray viewingRay = cam.calculateViewingRay(rowFrac, colFrac);
