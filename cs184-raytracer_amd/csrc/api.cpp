@@ -2,6 +2,7 @@
 // driver, PNG output.  This is the drop-in for Scene::renderScene (scene.cpp:10-59).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -63,7 +64,13 @@ struct rt_scene {
 	std::vector<unsigned long long> stats_host;
 	double* out_dev = nullptr;                   // staging for rt_render
 	int64_t out_capacity = 0;
-	hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // level stage boundaries
+	// Shading streams: k_shadow + k_shade of level L run on shade_streams[L % 2] while
+	// the render stream traces level L+1.
+	hipStream_t shade_streams[2] = {nullptr, nullptr};
+	// per level: [0] before k_closest, [1] after it (the shading streams wait on it),
+	// [2] before k_shadow, [3] after it, [4] after k_shade (the reduce waits on it)
+	std::vector<std::array<hipEvent_t, 5>> level_events;
+	int32_t* counts_host = nullptr;              // pinned: level counts + error word
 	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketShadow0;  // measured best on C3
 };
 
@@ -89,17 +96,17 @@ int ensure_level(rt_scene* s, size_t level, int64_t capacity) {
 	LevelBuffers& L = s->levels[level];
 	if (L.lv.capacity >= capacity) return RT_OK;
 	if (L.block) {
-		HIP_TRY(hipStreamSynchronize(s->stream));
+		HIP_TRY(hipDeviceSynchronize());
 		HIP_TRY(hipFree(L.block));
 		L.block = nullptr;
 	}
 	capacity = std::max<int64_t>(capacity, 1024);
 	const int64_t n = capacity;
 	const int64_t nl = std::max(8, s->ds.occl_stride);
-	// 18 double arrays, 4 int32 arrays, inside flags and n x lights shadow verdicts,
-	// each 256-B aligned
+	// 18 double arrays, 4 int32 arrays, inside flags, n x lights shadow verdicts and the
+	// level's counts, each 256-B aligned
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	const int64_t bytes = 18 * align(n * 8) + 4 * align(n * 4) + align(n) + align(n * nl);
+	const int64_t bytes = 18 * align(n * 8) + 4 * align(n * 4) + align(n) + align(n * nl) + 256;
 	HIP_TRY(hipMalloc(&L.block, bytes));
 	char* p = static_cast<char*>(L.block);
 	auto take = [&](int64_t b) {
@@ -116,7 +123,17 @@ int ensure_level(rt_scene* s, size_t level, int64_t capacity) {
 	L.lv.child_refl = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.inside = reinterpret_cast<uint8_t*>(take(n));
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
+	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
 	L.lv.capacity = capacity;
+	return RT_OK;
+}
+
+int ensure_events(rt_scene* s, size_t level) {
+	while (s->level_events.size() <= level) {
+		std::array<hipEvent_t, 5> ev{};
+		for (hipEvent_t& e : ev) HIP_TRY(hipEventCreate(&e));
+		s->level_events.push_back(ev);
+	}
 	return RT_OK;
 }
 
@@ -181,7 +198,8 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	s->device = device;
 	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);  // tuning knob
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-	for (hipEvent_t& e : s->ev) HIP_TRY(hipEventCreate(&e));
+	for (hipStream_t& q : s->shade_streams) HIP_TRY(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->counts_host), 4 * sizeof(int32_t), hipHostMallocDefault));
 	int rc;
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
@@ -226,14 +244,17 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 void rt_scene_destroy(rt_scene* s) {
 	if (!s) return;
 	(void)hipSetDevice(s->device);
-	if (s->stream) (void)hipStreamSynchronize(s->stream);
+	(void)hipDeviceSynchronize();
 	for (auto& L : s->levels)
 		if (L.block) (void)hipFree(L.block);
 	for (void* p : s->allocs) (void)hipFree(p);
 	if (s->out_dev) (void)hipFree(s->out_dev);
 	if (s->ctr_host) (void)hipHostFree(s->ctr_host);
-	for (hipEvent_t e : s->ev)
-		if (e) (void)hipEventDestroy(e);
+	if (s->counts_host) (void)hipHostFree(s->counts_host);
+	for (auto& ev : s->level_events)
+		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+	for (hipStream_t q : s->shade_streams)
+		if (q) (void)hipStreamDestroy(q);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
 	delete s;
 }
@@ -274,33 +295,72 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		fg.intersection_only = io;
 		level_n.assign(1, n0);
 		if ((rc = ensure_level(s, 0, n0))) return rc;
+		std::vector<int> shaded;  // levels whose shading was launched
+		bool error = false;
 		for (int L = 0;; L++) {
 			const int remaining = depth - L;
 			const int64_t n = level_n[L];
 			if (remaining > 0 && (rc = ensure_level(s, L + 1, 2 * n))) return rc;
-			HIP_TRY(hipMemsetAsync(&s->ctr->next_count, 0, sizeof(int32_t), st));
-			const rtamd::RayLevel& next = remaining > 0 ? s->levels[L + 1].lv : s->levels[L].lv;
-			HIP_TRY(rtamd::launch_level(s->ds, fg, L, n, remaining, s->levels[L].lv, next, s->ctr, s->stats, st,
-			                            s->ev, cnt.stage_launches, s->packet_mask));
-			HIP_TRY(hipMemcpyAsync(s->ctr_host, s->ctr, sizeof(rtamd::DeviceCounters), hipMemcpyDeviceToHost, st));
+			if ((rc = ensure_events(s, L))) return rc;
+			const auto& ev = s->level_events[L];
+			const rtamd::RayLevel& cur = s->levels[L].lv;
+			const rtamd::RayLevel& next = remaining > 0 ? s->levels[L + 1].lv : cur;
+			HIP_TRY(hipMemsetAsync(cur.counts, 0, 2 * sizeof(int32_t), st));
+			HIP_TRY(hipEventRecord(ev[0], st));
+			HIP_TRY(rtamd::launch_closest(s->ds, fg, L, n, remaining, cur, next, s->ctr, s->stats, st, s->packet_mask));
+			cnt.stage_launches[0]++;
+			HIP_TRY(hipEventRecord(ev[1], st));
+			HIP_TRY(hipMemcpyAsync(s->counts_host, cur.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+			HIP_TRY(hipMemcpyAsync(s->counts_host + 2, &s->ctr->error, sizeof(int32_t), hipMemcpyDeviceToHost, st));
 			HIP_TRY(hipStreamSynchronize(st));
-			for (int k = 0; k < 3; k++) {
-				float ms = 0.f;
-				HIP_TRY(hipEventElapsedTime(&ms, s->ev[k], s->ev[k + 1]));
-				cnt.stage_ms[k] += ms;
-				kernel_ms_total += ms;
+			if (s->counts_host[2]) {
+				error = true;
+				break;
 			}
-			if (s->ctr_host->error) break;
 			cnt.trace_rays += n;
-			const int64_t nn = s->ctr_host->next_count;
+			const int64_t nh = s->counts_host[0], nn = s->counts_host[1];
+			if (nh > 0) {  // shading of level L, concurrent with k_closest(L+1)
+				hipStream_t q = s->shade_streams[L % 2];
+				HIP_TRY(hipStreamWaitEvent(q, ev[1], 0));
+				HIP_TRY(hipEventRecord(ev[2], q));
+				HIP_TRY(rtamd::launch_shadow(s->ds, L, nh, cur, s->ctr, s->stats, q, s->packet_mask));
+				if (s->ds.n_nonambient > 0) cnt.stage_launches[1]++;
+				HIP_TRY(hipEventRecord(ev[3], q));
+				HIP_TRY(rtamd::launch_shade(s->ds, fg, L, nh, cur, s->ctr, q));
+				cnt.stage_launches[2]++;
+				HIP_TRY(hipEventRecord(ev[4], q));
+				shaded.push_back(L);
+			}
 			if (remaining <= 0 || nn == 0) break;
 			level_n.push_back(nn);
 		}
-		if (s->ctr_host->error) break;
+		if (error) {
+			HIP_TRY(hipDeviceSynchronize());
+			break;
+		}
+		for (int L : shaded) HIP_TRY(hipStreamWaitEvent(st, s->level_events[L][4], 0));
 		for (int L = static_cast<int>(level_n.size()) - 2; L >= 0; L--)
 			HIP_TRY(rtamd::launch_reduce_level(level_n[L], s->levels[L].lv, s->levels[L + 1].lv, st));
 		HIP_TRY(rtamd::launch_output(n0, s->levels[0].lv, out_rgb_dev ? out_rgb_dev + r0 * W * 3 : nullptr,
 		                             out_rgb8_dev ? out_rgb8_dev + r0 * W * 3 : nullptr, io, s->stats, st));
+		// per-kernel device times of this chunk (events are re-recorded by the next chunk)
+		HIP_TRY(hipStreamSynchronize(st));
+		for (int L = 0; L < static_cast<int>(level_n.size()); L++) {
+			const auto& ev = s->level_events[L];
+			float ms = 0.f;
+			HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
+			cnt.stage_ms[0] += ms;
+			kernel_ms_total += ms;
+		}
+		for (int L : shaded) {
+			const auto& ev = s->level_events[L];
+			for (int k = 0; k < 2; k++) {
+				float ms = 0.f;
+				HIP_TRY(hipEventElapsedTime(&ms, ev[2 + k], ev[3 + k]));
+				cnt.stage_ms[1 + k] += ms;
+				kernel_ms_total += ms;
+			}
+		}
 		cnt.levels = std::max<int32_t>(cnt.levels, static_cast<int32_t>(level_n.size()));
 		cnt.pixels += n0;
 	}

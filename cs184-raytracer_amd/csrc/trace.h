@@ -37,6 +37,7 @@ struct RayLevel {
 	double *cr, *cg, *cb;        // local colour, overwritten with the final colour by reduce
 	double *kr, *kg, *kb;        // reflective weight (after TIR), valid when child_refl >= 0
 	int32_t *child_refr, *child_refl;
+	int32_t* counts;             // [0] hits of this level (k_closest), [1] children spawned
 	int64_t capacity;
 };
 
@@ -47,14 +48,11 @@ struct FrameGeometry {
 	int32_t intersection_only;
 };
 
-// Device counters: first error code, next-level ray count, hits of the level being
-// traced (k_closest -> k_shadow), shaded hits (x non-ambient lights = shadow rays),
-// running max (bits) for --intersection-only, children spawned and work counters.
+// Device error word (first MathException code).  Ray and hit counts live per level
+// (RayLevel::counts) so that levels in flight on different streams never share one.
 struct DeviceCounters {
 	int32_t error;
-	int32_t next_count;
-	int32_t level_hits;
-	int32_t pad;
+	int32_t pad[3];
 };
 
 // Statistics are sharded: a single word takes only ~88 atomics/us on MI355X
@@ -69,14 +67,21 @@ enum StatSlot : int {
 };
 constexpr int kStatStride = 16;  // u64 per shard (128 B)
 
-// One wavefront level: closest hit, shadow rays, shading + children.  ev[0..3] (may be
-// null) are recorded on `stream` before k_closest and after each of the three kernels;
-// launches[k] counts the launches of kernel k.
+// Level pipeline.  k_closest(L) finds the closest hits of level L, appends the hits to
+// cur.hit_list (count cur.counts[0]) and spawns the reflection/refraction children into
+// `next` (count cur.counts[1]).  The shading of level L (shadow rays, then Phong terms)
+// depends only on k_closest(L), so it runs on a second stream while k_closest(L+1)
+// traces the children: the latency-bound deep levels overlap with shading work.
 // packet_mask selects wave-packet traversal per kernel and level class
 enum : int { kPacketClosest0 = 1, kPacketClosestN = 2, kPacketShadow0 = 4, kPacketShadowN = 8 };
-hipError_t launch_level(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
-                        const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
-                        hipStream_t stream, hipEvent_t* ev, int* launches, int packet_mask);
+hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
+                          const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
+                          hipStream_t stream, int packet_mask);
+// n_hits = cur.counts[0] (read back by the host after k_closest)
+hipError_t launch_shadow(const DeviceScene& s, int level, int64_t n_hits, const RayLevel& cur, DeviceCounters* ctr,
+                         unsigned long long* stats, hipStream_t stream, int packet_mask);
+hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n_hits, const RayLevel& cur,
+                        DeviceCounters* ctr, hipStream_t stream);
 hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream);
 hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8_t* out_rgb8,
                          int32_t intersection_only, unsigned long long* stats, hipStream_t stream);

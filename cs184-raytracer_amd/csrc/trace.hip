@@ -3,11 +3,12 @@
 // Wavefront formulation of the reference's recursive Scene::traceRay (scene.cpp:61-140).
 // Level L holds every ray of recursion depth L; per level three launches:
 //   k_closest  closest hit of every ray (castRay, scene.cpp:142-167); rays that hit are
-//              appended to a hit list (one atomic per wave)
+//              appended to a hit list, their refraction/reflection children to level L+1
+//              (scene.cpp:110-136), one atomic per block
 //   k_shadow   one lane per (hit, non-ambient light), light-major so a wave traces rays
 //              towards one light from neighbouring hits (scene.cpp:87-93)
-//   k_shade    Phong terms in light order + refraction/reflection children appended to
-//              level L+1 (scene.cpp:94-136)
+//   k_shade    Phong terms in light order (scene.cpp:78-108), one lane per hit
+// k_shadow/k_shade of level L run on a shading stream concurrently with k_closest(L+1).
 // then colours are reduced bottom-up (k_reduce) in the reference's addition order:
 // colour = (local + refraction) + reflection * kr (scene.cpp:127,134).
 // Device arithmetic: see intersect.h; pow is glibc's (glibc_pow.h).
@@ -20,7 +21,17 @@ namespace {
 
 using namespace dev;
 
-constexpr int kShadeBlock = 512;  // 8 waves: one child-allocation atomic per 512 rays
+constexpr int kShadeBlock = 512;
+
+// Occupancy target of the traversal kernels (waves per SIMD); 0 = compiler's choice.
+#ifndef RT_TRAVERSAL_WAVES
+#define RT_TRAVERSAL_WAVES 0
+#endif
+#if RT_TRAVERSAL_WAVES > 0
+#define RT_TRAVERSAL_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRAVERSAL_WAVES)))
+#else
+#define RT_TRAVERSAL_ATTR
+#endif  // 8 waves: one child-allocation atomic per 512 rays
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
 __device__ __forceinline__ void primary_ray(const DCamera& cam, int r, int c, int W, int H, V3& o, V3& d,
@@ -84,34 +95,50 @@ __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long l
 	}
 }
 
-// Block-wide append: this thread contributes `count` (0..2) slots; one atomicAdd per block
-// on *counter returns the block's base.  Every thread of the block must call it.
-// lds: kMaxWaves + 1 ints of shared memory.
+// Block-wide append to two counters: this thread contributes `a` (0/1) slots to counter
+// ca and `b0 + b1` (0..2) slots to counter cb; one atomicAdd per counter per block returns
+// the block's bases.  Every thread of the block must call it.
 constexpr int kMaxWaves = 16;
-__device__ __forceinline__ int block_append(bool a, bool b, int32_t* counter, int* lds) {
-	const unsigned long long ma = __ballot(a), mb = __ballot(b);
+struct AppendLds {
+	int n[2][kMaxWaves + 1];
+};
+struct Slots {
+	int a, b;
+};
+__device__ __forceinline__ Slots block_append2(bool a, bool b0, bool b1, int32_t* ca, int32_t* cb, AppendLds& lds) {
+	const unsigned long long ma = __ballot(a), m0 = __ballot(b0), m1 = __ballot(b1);
 	const int lane = __lane_id(), wave = threadIdx.x >> 6;
 	const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-	if (lane == 0) lds[wave] = __popcll(ma) + __popcll(mb);
+	if (lane == 0) {
+		lds.n[0][wave] = __popcll(ma);
+		lds.n[1][wave] = __popcll(m0) + __popcll(m1);
+	}
 	__syncthreads();
-	if (threadIdx.x == 0) {
+	if (threadIdx.x < 2) {
+		const int k = threadIdx.x;
 		const int nw = (blockDim.x + 63) >> 6;
 		int total = 0;
 		for (int w = 0; w < nw; w++) {
-			const int c = lds[w];
-			lds[w] = total;
+			const int c = lds.n[k][w];
+			lds.n[k][w] = total;
 			total += c;
 		}
-		lds[kMaxWaves] = total ? atomicAdd(counter, total) : 0;
+		lds.n[k][kMaxWaves] = total ? atomicAdd(k ? cb : ca, total) : 0;
 	}
 	__syncthreads();
-	return lds[kMaxWaves] + lds[wave] + __popcll(ma & below) + __popcll(mb & below);
+	return Slots{lds.n[0][kMaxWaves] + lds.n[0][wave] + (int)__popcll(ma & below),
+	             lds.n[1][kMaxWaves] + lds.n[1][wave] + (int)(__popcll(m0 & below) + __popcll(m1 & below))};
 }
 
+// Closest hit (castRay, scene.cpp:142-167) + the bounce decisions of scene.cpp:110-136:
+// the children's rays and the reflective weight depend only on the hit, not on the
+// shading, so they are spawned here and level L+1 can be traced while level L is shaded.
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, FrameGeometry fg, int level, int64_t n,
-                                                    RayLevel cur, DeviceCounters* ctr, unsigned long long* stats) {
-	__shared__ int append_lds[kMaxWaves + 1];
+__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScene S, FrameGeometry fg, int level,
+                                                                      int64_t n, int remaining, RayLevel cur,
+                                                                      RayLevel next, DeviceCounters* ctr,
+                                                                      unsigned long long* stats) {
+	__shared__ AppendLds append_lds;
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
 	const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -129,19 +156,54 @@ __global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, FrameGeometry
 		hit = closest_hit_packet(S, o, d, inside, active, dist, gi, P, Nobj, stack, ctr, ws);
 	else if (active)
 		hit = closest_hit(S, o, d, inside, dist, gi, P, Nobj, stack, ctr, ws);
+	flush_stats(ws, stats, 0);
 	if (hit) {
 		// Geometry::calculateIntersectionNormal tail (geometry.cpp:40-43) + scene.cpp:72-75
-		const auto G = uniform_ptr(S.geoms) + 0;
 		N = xf_normal(S.geoms[gi].inv, Nobj);
 		if (S.geoms[gi].flip) N = -N;
 		if (inside) N = -N;
 		const double rn = 1.0 / sqrt(sq4(N));  // targetNormal.normalize(): times 1/|N|
 		N = rn * N;
-		(void)G;
 	}
 	const bool shade = hit && !fg.intersection_only;
-	const int slot = block_append(shade, false, &ctr->level_hits, append_lds);
-	flush_stats(ws, stats, 0);
+	// bounce (scene.cpp:110-136): refraction first, then reflection with kr (1 on TIR)
+	double kr[3] = {0, 0, 0};
+	bool spawn_refr = false, spawn_refl = false;
+	V3 refr_d = mk(0, 0, 0), refl_d = mk(0, 0, 0);
+	if (shade && remaining > 0) {
+		const DMaterial& M = S.mats[S.geoms[gi].mat];
+		kr[0] = M.kr[0];
+		kr[1] = M.kr[1];
+		kr[2] = M.kr[2];
+		bool kr_nz = M.kr_nonzero;
+		if (M.kt_nonzero) {
+			const double nr = inside ? M.ior : 1.0 / M.ior;
+			const double cosI = dot4z(N, d);
+			const double sinT2 = nr * nr * (1.0 - cosI * cosI);
+			if (sinT2 > 1.0) {
+				kr[0] = kr[1] = kr[2] = 1.0;  // total internal reflection
+				kr_nz = true;
+			} else {
+				const double k2 = nr * cosI + sqrt(1.0 - sinT2);
+				refr_d = ray_dir(nr * d - k2 * N, ctr);
+				spawn_refr = true;
+			}
+		}
+		if (kr_nz) {
+			refl_d = ray_dir(d - (2 * dot4z(N, d)) * N, ctr);
+			spawn_refl = true;
+		}
+	}
+	const Slots slot = block_append2(shade, spawn_refr, spawn_refl, cur.counts, cur.counts + 1, append_lds);
+	{
+		const unsigned long long m_hit = __ballot(shade), m_refl = __ballot(spawn_refl), m_refr = __ballot(spawn_refr);
+		if (__lane_id() == 0) {
+			unsigned long long* sh = shard(stats);
+			if (m_hit) atomicAdd(sh + ST_HITS, (unsigned long long)__popcll(m_hit));
+			if (m_refl) atomicAdd(sh + ST_REFL, (unsigned long long)__popcll(m_refl));
+			if (m_refr) atomicAdd(sh + ST_REFR, (unsigned long long)__popcll(m_refr));
+		}
+	}
 	if (!active) return;
 	cur.hgeom[i] = hit ? gi : -1;
 	if (fg.intersection_only) {  // scene.cpp:69-70
@@ -150,27 +212,55 @@ __global__ void __launch_bounds__(kBlock) k_closest(DeviceScene S, FrameGeometry
 		cur.child_refr[i] = cur.child_refl[i] = -1;
 		return;
 	}
-	if (!hit) return;
+	int32_t refr_idx = -1, refl_idx = -1;
+	if (spawn_refr) {
+		refr_idx = slot.b;
+		next.ox[refr_idx] = P.x;
+		next.oy[refr_idx] = P.y;
+		next.oz[refr_idx] = P.z;
+		next.dx[refr_idx] = refr_d.x;
+		next.dy[refr_idx] = refr_d.y;
+		next.dz[refr_idx] = refr_d.z;
+		next.inside[refr_idx] = !inside;
+	}
+	if (spawn_refl) {
+		refl_idx = slot.b + (spawn_refr ? 1 : 0);
+		next.ox[refl_idx] = P.x;
+		next.oy[refl_idx] = P.y;
+		next.oz[refl_idx] = P.z;
+		next.dx[refl_idx] = refl_d.x;
+		next.dy[refl_idx] = refl_d.y;
+		next.dz[refl_idx] = refl_d.z;
+		next.inside[refl_idx] = inside;
+		cur.kr[i] = kr[0];
+		cur.kg[i] = kr[1];
+		cur.kb[i] = kr[2];
+	}
+	cur.child_refr[i] = refr_idx;
+	cur.child_refl[i] = refl_idx;
+	if (!hit) {  // background: black (scene.cpp:66-67); hits are coloured by k_shade
+		cur.cr[i] = cur.cg[i] = cur.cb[i] = 0.0;
+		return;
+	}
 	cur.hpx[i] = P.x;
 	cur.hpy[i] = P.y;
 	cur.hpz[i] = P.z;
 	cur.hnx[i] = N.x;
 	cur.hny[i] = N.y;
 	cur.hnz[i] = N.z;
-	cur.hit_list[slot] = (int32_t)i;
+	cur.hit_list[slot.a] = (int32_t)i;
 }
 
-// Shadow rays: item t -> (light j = t / hits, hit h = t % hits); grid sized for the
-// upper bound n * n_nonambient, the actual hit count is read from the counters.
+// Shadow rays: item t -> (light j = t / nh, hit h = t % nh), light-major so a wave traces
+// rays towards one light from neighbouring hits (scene.cpp:87-93).
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock) k_shadow(DeviceScene S, int level, RayLevel cur, DeviceCounters* ctr,
-                                                   unsigned long long* stats) {
+__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene S, int level, int64_t nh,
+                                                                     RayLevel cur, DeviceCounters* ctr,
+                                                                     unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	const int64_t nh = ctr->level_hits;
 	const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
 	const int nl = S.n_nonambient;
-	if ((int64_t)blockIdx.x * kBlock >= nh * nl) return;  // whole block idle (wave-uniform)
 	WorkStats ws{0, 0, 0, 0};
 	const bool on = t < nh * nl;
 	int32_t i = 0;
@@ -200,11 +290,9 @@ __global__ void __launch_bounds__(kBlock) k_shadow(DeviceScene S, int level, Ray
 	flush_stats(ws, stats, 1);
 }
 
-// Phong terms in light order (scene.cpp:78-108) + bounce (scene.cpp:110-136)
-__global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeometry fg, int level, int64_t n,
-                                                       int remaining, RayLevel cur, RayLevel next, DeviceCounters* ctr,
-                                                       unsigned long long* stats) {
-	__shared__ int append_lds[kMaxWaves + 1];
+// Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
+__global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeometry fg, int level, int64_t nh,
+                                                       RayLevel cur, DeviceCounters* ctr) {
 	// glibc pow tables in LDS: the specular pow's two dependent table lookups per light
 	// are LDS latency instead of divergent L2 gathers
 	__shared__ double log_tab[512];
@@ -213,115 +301,50 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	for (int k = threadIdx.x; k < 256; k += blockDim.x) exp_tab[k] = glibc_pow_data::kExpTab[k];
 	__syncthreads();
 	const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	const int64_t i = level == 0 ? tile_pixel(fg, n, t) : (t < n ? t : -1);
-	const bool active = i >= 0;
-	const int gi = active ? cur.hgeom[i] : -1;
+	if (t >= nh) return;
+	const int64_t i = cur.hit_list[t];
+	const int gi = cur.hgeom[i];
 	double col[3] = {0.0, 0.0, 0.0};
-	double kr[3] = {0, 0, 0};
-	bool spawn_refr = false, spawn_refl = false, inside = false;
-	V3 P = mk(0, 0, 0), refr_d = mk(0, 0, 0), refl_d = mk(0, 0, 0);
-	if (gi >= 0) {
-		V3 o, d;
-		level_ray(S, fg, level, i, cur, o, d, inside, ctr);
-		P = mk(cur.hpx[i], cur.hpy[i], cur.hpz[i]);
-		const V3 N = mk(cur.hnx[i], cur.hny[i], cur.hnz[i]);
-		const DMaterial& M = S.mats[S.geoms[gi].mat];
-		const uint64_t* occ_words = reinterpret_cast<const uint64_t*>(cur.occl + i * S.occl_stride);
-		uint64_t occ_word = 0;
-		int j = 0;
-		for (int li = 0; li < S.n_lights; li++) {
-			const DLight& L = S.lights[li];
-			if (L.kind == DLIGHT_AMBIENT) {
+	V3 o, d;
+	bool inside;
+	level_ray(S, fg, level, i, cur, o, d, inside, ctr);
+	const V3 P = mk(cur.hpx[i], cur.hpy[i], cur.hpz[i]);
+	const V3 N = mk(cur.hnx[i], cur.hny[i], cur.hnz[i]);
+	const DMaterial& M = S.mats[S.geoms[gi].mat];
+	const uint64_t* occ_words = reinterpret_cast<const uint64_t*>(cur.occl + i * S.occl_stride);
+	uint64_t occ_word = 0;
+	int j = 0;
+	for (int li = 0; li < S.n_lights; li++) {
+		const DLight& L = S.lights[li];
+		if (L.kind == DLIGHT_AMBIENT) {
 #pragma unroll
-				for (int k = 0; k < 3; k++) col[k] = col[k] + (1.0 * L.color[k]) * M.ka[k];
-				continue;
-			}
-			if ((j & 7) == 0) occ_word = occ_words[j >> 3];
-			const bool occ = (occ_word >> (8 * (j & 7))) & 0xff;
-			j++;
-			if (occ) continue;
-			const bool point = L.kind == DLIGHT_POINT;
-			const V3 lv = load3(L.vec);
-			const V3 Ld = ray_dir(point ? lv - P : -lv, ctr);
-			const double nl_dot = dot4z(N, Ld);
-			const double dL = point ? sqrt(sq4(lv - P)) : INFINITY;
-			const double fall = point ? glibc_pow(dL, -L.falloff, log_tab, exp_tab) : 1.0;  // colorForDistance
-			double att[3];
-#pragma unroll
-			for (int k = 0; k < 3; k++) att[k] = point ? fall * L.color[k] : L.color[k];
-			const double diff = max0(nl_dot);
-#pragma unroll
-			for (int k = 0; k < 3; k++) col[k] = col[k] + (diff * att[k]) * M.kd[k];
-			const V3 R = (2 * nl_dot) * N - Ld;
-			const double spec = glibc_pow(max0(-dot4z(d, R)), M.ns, log_tab, exp_tab);
-#pragma unroll
-			for (int k = 0; k < 3; k++) col[k] = col[k] + (spec * att[k]) * M.ks[k];
+			for (int k = 0; k < 3; k++) col[k] = col[k] + (1.0 * L.color[k]) * M.ka[k];
+			continue;
 		}
-		if (remaining > 0) {
-			kr[0] = M.kr[0];
-			kr[1] = M.kr[1];
-			kr[2] = M.kr[2];
-			bool kr_nz = M.kr_nonzero;
-			if (M.kt_nonzero) {
-				const double nr = inside ? M.ior : 1.0 / M.ior;
-				const double cosI = dot4z(N, d);
-				const double sinT2 = nr * nr * (1.0 - cosI * cosI);
-				if (sinT2 > 1.0) {
-					kr[0] = kr[1] = kr[2] = 1.0;  // total internal reflection
-					kr_nz = true;
-				} else {
-					const double k2 = nr * cosI + sqrt(1.0 - sinT2);
-					refr_d = ray_dir(nr * d - k2 * N, ctr);
-					spawn_refr = true;
-				}
-			}
-			if (kr_nz) {
-				refl_d = ray_dir(d - (2 * dot4z(N, d)) * N, ctr);
-				spawn_refl = true;
-			}
-		}
-	}
-	// children -> level + 1 (one atomic per block); statistics into a shard
-	const int slot = block_append(spawn_refr, spawn_refl, &ctr->next_count, append_lds);
-	{
-		const unsigned long long m_hit = __ballot(gi >= 0), m_refl = __ballot(spawn_refl), m_refr = __ballot(spawn_refr);
-		if (__lane_id() == 0) {
-			unsigned long long* sh = shard(stats);
-			if (m_hit) atomicAdd(sh + ST_HITS, (unsigned long long)__popcll(m_hit));
-			if (m_refl) atomicAdd(sh + ST_REFL, (unsigned long long)__popcll(m_refl));
-			if (m_refr) atomicAdd(sh + ST_REFR, (unsigned long long)__popcll(m_refr));
-		}
-	}
-	if (!active) return;
-	int32_t refr_idx = -1, refl_idx = -1;
-	if (spawn_refr) {
-		refr_idx = slot;
-		next.ox[refr_idx] = P.x;
-		next.oy[refr_idx] = P.y;
-		next.oz[refr_idx] = P.z;
-		next.dx[refr_idx] = refr_d.x;
-		next.dy[refr_idx] = refr_d.y;
-		next.dz[refr_idx] = refr_d.z;
-		next.inside[refr_idx] = !inside;
-	}
-	if (spawn_refl) {
-		refl_idx = slot + (spawn_refr ? 1 : 0);
-		next.ox[refl_idx] = P.x;
-		next.oy[refl_idx] = P.y;
-		next.oz[refl_idx] = P.z;
-		next.dx[refl_idx] = refl_d.x;
-		next.dy[refl_idx] = refl_d.y;
-		next.dz[refl_idx] = refl_d.z;
-		next.inside[refl_idx] = inside;
-		cur.kr[i] = kr[0];
-		cur.kg[i] = kr[1];
-		cur.kb[i] = kr[2];
+		if ((j & 7) == 0) occ_word = occ_words[j >> 3];
+		const bool occ = (occ_word >> (8 * (j & 7))) & 0xff;
+		j++;
+		if (occ) continue;
+		const bool point = L.kind == DLIGHT_POINT;
+		const V3 lv = load3(L.vec);
+		const V3 Ld = ray_dir(point ? lv - P : -lv, ctr);
+		const double nl_dot = dot4z(N, Ld);
+		const double dL = point ? sqrt(sq4(lv - P)) : INFINITY;
+		const double fall = point ? glibc_pow(dL, -L.falloff, log_tab, exp_tab) : 1.0;  // colorForDistance
+		double att[3];
+#pragma unroll
+		for (int k = 0; k < 3; k++) att[k] = point ? fall * L.color[k] : L.color[k];
+		const double diff = max0(nl_dot);
+#pragma unroll
+		for (int k = 0; k < 3; k++) col[k] = col[k] + (diff * att[k]) * M.kd[k];
+		const V3 R = (2 * nl_dot) * N - Ld;
+		const double spec = glibc_pow(max0(-dot4z(d, R)), M.ns, log_tab, exp_tab);
+#pragma unroll
+		for (int k = 0; k < 3; k++) col[k] = col[k] + (spec * att[k]) * M.ks[k];
 	}
 	cur.cr[i] = col[0];
 	cur.cg[i] = col[1];
 	cur.cb[i] = col[2];
-	cur.child_refr[i] = refr_idx;
-	cur.child_refl[i] = refl_idx;
 }
 
 // colour = (local + refraction) + reflection * kr, in place (scene.cpp:127,134)
@@ -406,42 +429,39 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 
 }  // namespace
 
-hipError_t launch_level(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
-                        const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
-                        hipStream_t stream, hipEvent_t* ev, int* launches, int packet_mask) {
+hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
+                          const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
+                          hipStream_t stream, int packet_mask) {
 	if (n <= 0) return hipSuccess;
-	hipError_t e;
-	if ((e = hipMemsetAsync(&ctr->level_hits, 0, sizeof(int32_t), stream)) != hipSuccess) return e;
-	if (ev && (e = hipEventRecord(ev[0], stream)) != hipSuccess) return e;
-	const bool pc = packet_mask & (level == 0 ? kPacketClosest0 : kPacketClosestN);
-	if (pc) {
+	if (packet_mask & (level == 0 ? kPacketClosest0 : kPacketClosestN)) {
 		const int64_t threads = level == 0 ? tile_threads(n, fg.width) : n;
 		hipLaunchKernelGGL(k_closest<true>, dim3(grid_for(threads, kBlock)), dim3(kBlock), 0, stream, s, fg, level, n,
-		                   cur, ctr, stats);
+		                   remaining_depth, cur, next, ctr, stats);
 	} else {
-		hipLaunchKernelGGL(k_closest<false>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, stream, s, fg, level, n, cur,
+		hipLaunchKernelGGL(k_closest<false>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, stream, s, fg, level, n,
+		                   remaining_depth, cur, next, ctr, stats);
+	}
+	return hipGetLastError();
+}
+
+hipError_t launch_shadow(const DeviceScene& s, int level, int64_t n_hits, const RayLevel& cur, DeviceCounters* ctr,
+                         unsigned long long* stats, hipStream_t stream, int packet_mask) {
+	const int64_t items = n_hits * s.n_nonambient;
+	if (items <= 0) return hipSuccess;
+	if (packet_mask & (level == 0 ? kPacketShadow0 : kPacketShadowN))
+		hipLaunchKernelGGL(k_shadow<true>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, level, n_hits, cur,
 		                   ctr, stats);
-	}
-	launches[0]++;
-	if (ev && (e = hipEventRecord(ev[1], stream)) != hipSuccess) return e;
-	if (!fg.intersection_only && s.n_nonambient > 0) {
-		const bool ps = packet_mask & (level == 0 ? kPacketShadow0 : kPacketShadowN);
-		if (ps)
-			hipLaunchKernelGGL(k_shadow<true>, dim3(grid_for(n * s.n_nonambient, kBlock)), dim3(kBlock), 0, stream, s,
-			                   level, cur, ctr, stats);
-		else
-			hipLaunchKernelGGL(k_shadow<false>, dim3(grid_for(n * s.n_nonambient, kBlock)), dim3(kBlock), 0, stream, s,
-			                   level, cur, ctr, stats);
-		launches[1]++;
-	}
-	if (ev && (e = hipEventRecord(ev[2], stream)) != hipSuccess) return e;
-	if (!fg.intersection_only) {
-		const int64_t threads = level == 0 ? tile_threads(n, fg.width) : n;
-		hipLaunchKernelGGL(k_shade, dim3(grid_for(threads, kShadeBlock)), dim3(kShadeBlock), 0, stream, s, fg, level,
-		                   n, remaining_depth, cur, next, ctr, stats);
-		launches[2]++;
-	}
-	if (ev && (e = hipEventRecord(ev[3], stream)) != hipSuccess) return e;
+	else
+		hipLaunchKernelGGL(k_shadow<false>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, level, n_hits,
+		                   cur, ctr, stats);
+	return hipGetLastError();
+}
+
+hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n_hits, const RayLevel& cur,
+                        DeviceCounters* ctr, hipStream_t stream) {
+	if (n_hits <= 0) return hipSuccess;
+	hipLaunchKernelGGL(k_shade, dim3(grid_for(n_hits, kShadeBlock)), dim3(kShadeBlock), 0, stream, s, fg, level, n_hits,
+	                   cur, ctr);
 	return hipGetLastError();
 }
 

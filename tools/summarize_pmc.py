@@ -8,7 +8,7 @@ import sys
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in sys.argv[1:]:
     for r in csv.DictReader(open(path)):
-        m = re.search(r"(k_[a-z0-9_]+)\(", r["Kernel_Name"])
+        m = re.search(r"(k_[a-z0-9_]+(?:<[a-z]+>)?)\(", r["Kernel_Name"])
         name = m.group(1) if m else r["Kernel_Name"][:24]
         acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in sorted(acc.items()):
