@@ -64,9 +64,10 @@ struct rt_scene {
 	std::vector<unsigned long long> stats_host;
 	double* out_dev = nullptr;                   // staging for rt_render
 	int64_t out_capacity = 0;
-	// Shading streams: k_shadow + k_shade of level L run on shade_streams[L % 2] while
-	// the render stream traces level L+1.
-	hipStream_t shade_streams[2] = {nullptr, nullptr};
+	// Shading streams: k_shadow + k_shade of level L run on shade_streams[L % 4] while
+	// the render stream (high priority: it carries the critical path) traces level L+1.
+	hipStream_t shade_streams[4] = {nullptr, nullptr, nullptr, nullptr};
+	hipEvent_t fork_event = nullptr;             // caller's stream -> render stream
 	// per level: [0] before k_closest, [1] after it (the shading streams wait on it),
 	// [2] before k_shadow, [3] after it, [4] after k_shade (the reduce waits on it)
 	std::vector<std::array<hipEvent_t, 5>> level_events;
@@ -197,8 +198,11 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	std::unique_ptr<rt_scene> s(new rt_scene());
 	s->device = device;
 	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);  // tuning knob
-	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-	for (hipStream_t& q : s->shade_streams) HIP_TRY(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+	int prio_low = 0, prio_high = 0;
+	HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_low, &prio_high));
+	HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_high));
+	for (hipStream_t& q : s->shade_streams) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
+	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
 	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->counts_host), 4 * sizeof(int32_t), hipHostMallocDefault));
 	int rc;
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
@@ -255,6 +259,7 @@ void rt_scene_destroy(rt_scene* s) {
 		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 	for (hipStream_t q : s->shade_streams)
 		if (q) (void)hipStreamDestroy(q);
+	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
 	delete s;
 }
@@ -270,7 +275,15 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 	int rc = check_params(s, p);
 	if (rc) return rc;
 	HIP_TRY(hipSetDevice(s->device));
-	hipStream_t st = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
+	// All work runs on the scene's streams; a caller's stream is joined first (its prior
+	// work, e.g. the allocation of the output buffers, completes before ours starts) and
+	// the call returns after the render stream has drained.
+	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
+	hipStream_t st = s->stream;
+	if (caller != st) {
+		HIP_TRY(hipEventRecord(s->fork_event, caller));
+		HIP_TRY(hipStreamWaitEvent(st, s->fork_event, 0));
+	}
 	const int64_t W = p->width;
 	const int64_t n_rows = selected_rows(p);
 	const int io = p->intersection_only != 0;
@@ -320,7 +333,7 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 			cnt.trace_rays += n;
 			const int64_t nh = s->counts_host[0], nn = s->counts_host[1];
 			if (nh > 0) {  // shading of level L, concurrent with k_closest(L+1)
-				hipStream_t q = s->shade_streams[L % 2];
+				hipStream_t q = s->shade_streams[L % 4];
 				HIP_TRY(hipStreamWaitEvent(q, ev[1], 0));
 				HIP_TRY(hipEventRecord(ev[2], q));
 				HIP_TRY(rtamd::launch_shadow(s->ds, L, nh, cur, s->ctr, s->stats, q, s->packet_mask));

@@ -20,7 +20,16 @@
 namespace rtamd {
 namespace dev {
 
-constexpr int kBlock = 128;  // 2 waves; LDS traversal stack = kStackDepth x kBlock x 4 B
+constexpr int kBlock = 128;  // 2 waves; LDS traversal stack = kStackDepth x kBlock x (4 + 4) B
+
+#ifndef RT_WHILE_WHILE
+#define RT_WHILE_WHILE 1
+#endif
+// per-lane traversal stack words per entry: node ref (+ entry distance with RT_POP_PRUNE)
+#ifndef RT_POP_PRUNE
+#define RT_POP_PRUNE 0
+#endif
+constexpr int kStackWords = (RT_WHILE_WHILE && RT_POP_PRUNE) ? 2 : 1;
 
 // Scene data read at a wave-uniform address goes through the constant address space so
 // it is fetched with scalar (SMEM) loads into SGPRs: one fetch per wave, no VGPRs.
@@ -230,6 +239,71 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 				return true;
 			}
 	} else {
+#if RT_WHILE_WHILE
+		// while-while traversal (Aila & Laine 2009): a lane first walks inner nodes until
+		// it holds a leaf, then the lanes holding leaves test their faces together, so
+		// node and face work do not interleave within a wave.  `ref` >= 0 is a node,
+		// <= -2 a leaf (face offset << 3 | count), -1 done.  The stack keeps each far
+		// child's entry distance (rounded down to float) so that a popped subtree the
+		// search has since pruned (it begins beyond the best face) is skipped.
+		const V3 inv = safe_inv(d);
+		float* tstack = reinterpret_cast<float*>(stack + kStackDepth * kBlock);
+		(void)tstack;
+		int32_t ref = G->bvh_root;
+		int sp = 0;
+		auto pop = [&]() {
+#if RT_POP_PRUNE
+			const double lim = fmin(prune_limit(best.dist), prune_cap);
+			while (sp > 0) {
+				--sp;
+				if ((double)tstack[sp * kBlock] <= lim) return stack[sp * kBlock];
+			}
+			return (int32_t)-1;
+#else
+			return sp > 0 ? stack[--sp * kBlock] : (int32_t)-1;
+#endif
+		};
+		while (ref != -1) {
+			while (ref >= 0) {
+				ws.nodes++;
+				const DBvhNode* N = S.nodes + ref;
+				double tn0, tn1;
+				const double lim = fmin(prune_limit(best.dist), prune_cap);
+				const bool h0 = slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
+				const bool h1 = slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+				if (h0 || h1) {
+					const int c = (h0 && h1) ? (tn1 < tn0 ? 1 : 0) : (h1 ? 1 : 0);
+					const int32_t cf = N->first[c], cc = N->count[c];
+					const int32_t near_ref = cc > 0 ? -2 - ((cf << 3) | cc) : cf;
+					if (h0 && h1) {
+						const int32_t ff = N->first[c ^ 1], fc = N->count[c ^ 1];
+						if (sp < kStackDepth) {
+							stack[sp * kBlock] = fc > 0 ? -2 - ((ff << 3) | fc) : ff;
+#if RT_POP_PRUNE
+							tstack[sp * kBlock] = __double2float_rd(c ? tn0 : tn1);
+#endif
+							sp++;
+						} else {
+							raise_error(ctr, DERR_STACK);
+						}
+					}
+					ref = near_ref;
+				} else {
+					ref = pop();
+				}
+			}
+			if (ref == -1) break;
+			const int32_t code = -2 - ref;
+			const int32_t f0 = G->face_begin + (code >> 3), f1 = f0 + (code & 7);
+			for (int32_t f = f0; f < f1; f++)
+				if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+					settled = true;
+					return true;
+				}
+			ref = pop();
+		}
+	}
+#else
 		const V3 inv = safe_inv(d);
 		int32_t node = G->bvh_root;
 		int sp = 0;
@@ -270,6 +344,7 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 			node = next;
 		}
 	}
+#endif
 	found_dist = best.dist;
 	if (best.face < 0) return false;
 	const DFaceGeo* F = S.fgeo + best.face;

@@ -75,6 +75,23 @@ __host__ __device__ __forceinline__ int64_t tile_threads(int64_t n, int64_t widt
 	return ((width + 7) / 8) * ((n / width + 7) / 8) * 64;
 }
 
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup
+// dispatch"), each with its own 4 MiB L2.  The logical block index gives XCD x (blocks
+// b = x mod 8) runs of RT_XCD_GROUP consecutive blocks, so the rays one L2 serves at a
+// time are neighbours and share BVH nodes and triangles, while every XCD still sweeps the
+// whole image (balanced load).  Speed only: any bijection is correct.
+#ifndef RT_XCD_GROUP
+#define RT_XCD_GROUP 0
+#endif
+__device__ __forceinline__ int64_t xcd_block() {
+	const int64_t nb = gridDim.x, b = blockIdx.x;
+	if (RT_XCD_GROUP <= 0) return b;
+	constexpr int64_t g = RT_XCD_GROUP, span = 8 * g;
+	const int64_t base = (b / span) * span;
+	if (base + span > nb) return b;  // tail: identity
+	return base + (b & 7) * g + ((b - base) >> 3);
+}
+
 // std::max(x, 0.0)
 __device__ __forceinline__ double max0(double x) { return (x < 0.0) ? 0.0 : x; }
 
@@ -139,9 +156,9 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScen
                                                                       RayLevel next, DeviceCounters* ctr,
                                                                       unsigned long long* stats) {
 	__shared__ AppendLds append_lds;
-	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackWords * kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+	const int64_t t = xcd_block() * kBlock + threadIdx.x;
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
 	WorkStats ws{0, 0, 0, 0};
@@ -257,9 +274,9 @@ template <bool kPacket>
 __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene S, int level, int64_t nh,
                                                                      RayLevel cur, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
-	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackWords * kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+	const int64_t t = xcd_block() * kBlock + threadIdx.x;
 	const int nl = S.n_nonambient;
 	WorkStats ws{0, 0, 0, 0};
 	const bool on = t < nh * nl;
@@ -300,7 +317,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	for (int k = threadIdx.x; k < 512; k += blockDim.x) log_tab[k] = glibc_pow_data::kLogTab[k];
 	for (int k = threadIdx.x; k < 256; k += blockDim.x) exp_tab[k] = glibc_pow_data::kExpTab[k];
 	__syncthreads();
-	const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	const int64_t t = xcd_block() * blockDim.x + threadIdx.x;
 	if (t >= nh) return;
 	const int64_t i = cur.hit_list[t];
 	const int gi = cur.hgeom[i];
