@@ -64,12 +64,20 @@ struct rt_scene {
 	std::vector<unsigned long long> stats_host;
 	double* out_dev = nullptr;                   // staging for rt_render
 	int64_t out_capacity = 0;
-	// Shading streams: k_shadow + k_shade of level L run on shade_streams[L % 4] while
-	// the render stream (high priority: it carries the critical path) traces level L+1.
+	// Shading streams: k_shadow + k_shade of level L < direct_levels run on
+	// shade_streams[L % 3] while the render stream (high priority: it carries the critical
+	// path) traces level L+1; the deeper, smaller levels are shaded together in batches on
+	// shade_streams[3] once the closest-hit chain has finished.
 	hipStream_t shade_streams[4] = {nullptr, nullptr, nullptr, nullptr};
+	int direct_levels = 3;
+	// RayLevel records of all levels for the batched shading kernels (pinned + device)
+	rtamd::RayLevel* levels_pinned = nullptr;
+	rtamd::RayLevel* levels_dev = nullptr;
+	size_t levels_cap = 0;
 	hipEvent_t fork_event = nullptr;             // caller's stream -> render stream
-	// per level: [0] before k_closest, [1] after it (the shading streams wait on it),
-	// [2] before k_shadow, [3] after it, [4] after k_shade (the reduce waits on it)
+	// per level: [0] before k_closest, [1] after it (the shading streams wait on it);
+	// per shading launch, in the events of its first level: [2] before k_shadow, [3] after
+	// it, [4] after k_shade (the reduce waits on it)
 	std::vector<std::array<hipEvent_t, 5>> level_events;
 	int32_t* counts_host = nullptr;              // pinned: level counts + error word
 	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketShadow0;  // measured best on C3
@@ -126,6 +134,30 @@ int ensure_level(rt_scene* s, size_t level, int64_t capacity) {
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
 	L.lv.capacity = capacity;
+	return RT_OK;
+}
+
+// Level `level` exists and its RayLevel record is in the pinned array (the record of an
+// earlier level never changes while copies of it may be in flight).
+int ensure_level_record(rt_scene* s, size_t level, int64_t capacity) {
+	if (level + 1 > s->levels_cap) {
+		HIP_TRY(hipDeviceSynchronize());
+		const size_t cap = std::max<size_t>(16, 2 * (level + 1));
+		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
+		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), hipHostMallocDefault));
+		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dev), cap * sizeof(rtamd::RayLevel)));
+		if (s->levels_pinned) {
+			std::memcpy(pin, s->levels_pinned, s->levels_cap * sizeof(rtamd::RayLevel));
+			(void)hipHostFree(s->levels_pinned);
+			(void)hipFree(s->levels_dev);
+		}
+		s->levels_pinned = pin;
+		s->levels_dev = dev;
+		s->levels_cap = cap;
+	}
+	int rc = ensure_level(s, level, capacity);
+	if (rc) return rc;
+	s->levels_pinned[level] = s->levels[level].lv;
 	return RT_OK;
 }
 
@@ -197,7 +229,8 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
 	std::unique_ptr<rt_scene> s(new rt_scene());
 	s->device = device;
-	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);  // tuning knob
+	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);  // tuning knobs
+	if (const char* dl = std::getenv("RTAMD_DIRECT_LEVELS")) s->direct_levels = std::max(1, std::atoi(dl));
 	int prio_low = 0, prio_high = 0;
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_low, &prio_high));
 	HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_high));
@@ -255,6 +288,8 @@ void rt_scene_destroy(rt_scene* s) {
 	if (s->out_dev) (void)hipFree(s->out_dev);
 	if (s->ctr_host) (void)hipHostFree(s->ctr_host);
 	if (s->counts_host) (void)hipHostFree(s->counts_host);
+	if (s->levels_pinned) (void)hipHostFree(s->levels_pinned);
+	if (s->levels_dev) (void)hipFree(s->levels_dev);
 	for (auto& ev : s->level_events)
 		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 	for (hipStream_t q : s->shade_streams)
@@ -307,13 +342,46 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		fg.chunk_row0 = static_cast<int32_t>(r0);
 		fg.intersection_only = io;
 		level_n.assign(1, n0);
-		if ((rc = ensure_level(s, 0, n0))) return rc;
-		std::vector<int> shaded;  // levels whose shading was launched
+		if ((rc = ensure_level_record(s, 0, n0))) return rc;
+		std::vector<int> shaded;                            // first level of each shading launch
+		std::vector<std::pair<int, int64_t>> deferred;      // (level, hits) shaded after the chain
+		// k_shadow + k_shade of the levels `lv` (their k_closest done) on stream q
+		auto launch_shading = [&](const std::vector<std::pair<int, int64_t>>& lv, hipStream_t q) -> int {
+			rtamd::ShadeBatch b{};
+			const int64_t nl = s->ds.n_nonambient;
+			auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
+			int64_t so = 0, ho = 0;
+			b.n = static_cast<int32_t>(lv.size());
+			for (int k = 0; k < b.n; k++) {
+				b.level[k] = lv[k].first;
+				b.nh[k] = lv[k].second;
+				b.shadow_begin[k] = so;
+				b.shade_begin[k] = ho;
+				so += wave_up(lv[k].second * nl);
+				ho += wave_up(lv[k].second);
+			}
+			b.shadow_begin[b.n] = so;
+			b.shade_begin[b.n] = ho;
+			const int first = lv.front().first, last = lv.back().first;
+			const auto& ev = s->level_events[first];
+			HIP_TRY(hipStreamWaitEvent(q, s->level_events[last][1], 0));
+			HIP_TRY(hipMemcpyAsync(s->levels_dev, s->levels_pinned, (last + 1) * sizeof(rtamd::RayLevel),
+			                       hipMemcpyHostToDevice, q));
+			HIP_TRY(hipEventRecord(ev[2], q));
+			HIP_TRY(rtamd::launch_shadow(s->ds, b, s->levels_dev, s->ctr, s->stats, q, s->packet_mask));
+			if (nl > 0) cnt.stage_launches[1]++;
+			HIP_TRY(hipEventRecord(ev[3], q));
+			HIP_TRY(rtamd::launch_shade(s->ds, fg, b, s->levels_dev, s->ctr, q));
+			cnt.stage_launches[2]++;
+			HIP_TRY(hipEventRecord(ev[4], q));
+			shaded.push_back(first);
+			return RT_OK;
+		};
 		bool error = false;
 		for (int L = 0;; L++) {
 			const int remaining = depth - L;
 			const int64_t n = level_n[L];
-			if (remaining > 0 && (rc = ensure_level(s, L + 1, 2 * n))) return rc;
+			if (remaining > 0 && (rc = ensure_level_record(s, L + 1, 2 * n))) return rc;
 			if ((rc = ensure_events(s, L))) return rc;
 			const auto& ev = s->level_events[L];
 			const rtamd::RayLevel& cur = s->levels[L].lv;
@@ -332,17 +400,12 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 			}
 			cnt.trace_rays += n;
 			const int64_t nh = s->counts_host[0], nn = s->counts_host[1];
-			if (nh > 0) {  // shading of level L, concurrent with k_closest(L+1)
-				hipStream_t q = s->shade_streams[L % 4];
-				HIP_TRY(hipStreamWaitEvent(q, ev[1], 0));
-				HIP_TRY(hipEventRecord(ev[2], q));
-				HIP_TRY(rtamd::launch_shadow(s->ds, L, nh, cur, s->ctr, s->stats, q, s->packet_mask));
-				if (s->ds.n_nonambient > 0) cnt.stage_launches[1]++;
-				HIP_TRY(hipEventRecord(ev[3], q));
-				HIP_TRY(rtamd::launch_shade(s->ds, fg, L, nh, cur, s->ctr, q));
-				cnt.stage_launches[2]++;
-				HIP_TRY(hipEventRecord(ev[4], q));
-				shaded.push_back(L);
+			if (nh > 0) {
+				if (L < s->direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
+					if ((rc = launch_shading({{L, nh}}, s->shade_streams[L % 3]))) return rc;
+				} else {
+					deferred.push_back({L, nh});
+				}
 			}
 			if (remaining <= 0 || nn == 0) break;
 			level_n.push_back(nn);
@@ -350,6 +413,10 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		if (error) {
 			HIP_TRY(hipDeviceSynchronize());
 			break;
+		}
+		for (size_t k = 0; k < deferred.size(); k += rtamd::kMaxBatch) {
+			const size_t e = std::min(deferred.size(), k + rtamd::kMaxBatch);
+			if ((rc = launch_shading({deferred.begin() + k, deferred.begin() + e}, s->shade_streams[3]))) return rc;
 		}
 		for (int L : shaded) HIP_TRY(hipStreamWaitEvent(st, s->level_events[L][4], 0));
 		for (int L = static_cast<int>(level_n.size()) - 2; L >= 0; L--)

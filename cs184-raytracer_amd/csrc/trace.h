@@ -77,10 +77,20 @@ enum : int { kPacketClosest0 = 1, kPacketClosestN = 2, kPacketShadow0 = 4, kPack
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
                           const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
                           hipStream_t stream, int packet_mask);
-// n_hits = cur.counts[0] (read back by the host after k_closest)
-hipError_t launch_shadow(const DeviceScene& s, int level, int64_t n_hits, const RayLevel& cur, DeviceCounters* ctr,
+// Shading of one or more levels in one launch (the deep levels are shaded together once
+// the closest-hit chain has finished).  Items of each level start on a wave boundary so
+// that every wave belongs to one level.  levels_dev: device copy of the RayLevel records.
+constexpr int kMaxBatch = 16;
+struct ShadeBatch {
+	int32_t n;                           // levels in the batch
+	int32_t level[kMaxBatch];
+	int64_t nh[kMaxBatch];               // hits of each level (cur.counts[0])
+	int64_t shadow_begin[kMaxBatch + 1]; // k_shadow item ranges: nh * n_nonambient each
+	int64_t shade_begin[kMaxBatch + 1];  // k_shade item ranges: nh each
+};
+hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
                          unsigned long long* stats, hipStream_t stream, int packet_mask);
-hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n_hits, const RayLevel& cur,
+hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
                         DeviceCounters* ctr, hipStream_t stream);
 hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream);
 hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8_t* out_rgb8,

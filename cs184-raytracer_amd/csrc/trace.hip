@@ -47,8 +47,9 @@ __device__ __forceinline__ void primary_ray(const DCamera& cam, int r, int c, in
 	d = ray_dir(mk(p[0] - cam.eye[0], p[1] - cam.eye[1], p[2] - cam.eye[2]), ctr);
 }
 
+template <typename LV>
 __device__ __forceinline__ void level_ray(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t i,
-                                          const RayLevel& cur, V3& o, V3& d, bool& inside, DeviceCounters* ctr) {
+                                          const LV& cur, V3& o, V3& d, bool& inside, DeviceCounters* ctr) {
 	if (level == 0) {
 		const int64_t row_ord = fg.chunk_row0 + i / fg.width;
 		const int r = fg.row_begin + (int)row_ord * fg.row_step;
@@ -268,15 +269,33 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScen
 	cur.hit_list[slot.a] = (int32_t)i;
 }
 
-// Shadow rays: item t -> (light j = t / nh, hit h = t % nh), light-major so a wave traces
-// rays towards one light from neighbouring hits (scene.cpp:87-93).
+// Level of item t of a batch (wave-uniform: every level's items start on a wave boundary)
+struct BatchItem {
+	int32_t level;
+	int64_t local, nh;
+};
+__device__ __forceinline__ BatchItem batch_item(const ShadeBatch& B, const int64_t* begin, int64_t t) {
+	BatchItem r{B.level[0], t - begin[0], B.nh[0]};
+#pragma unroll
+	for (int k = 1; k < kMaxBatch; k++)
+		if (k < B.n && t >= begin[k]) r = BatchItem{B.level[k], t - begin[k], B.nh[k]};
+	r.level = __builtin_amdgcn_readfirstlane(r.level);
+	return r;
+}
+
+// Shadow rays: item t of a level -> (light j = t / nh, hit h = t % nh), light-major so a
+// wave traces rays towards one light from neighbouring hits (scene.cpp:87-93).
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene S, int level, int64_t nh,
-                                                                     RayLevel cur, DeviceCounters* ctr,
+__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene S, ShadeBatch B,
+                                                                     const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackWords * kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	const int64_t t = xcd_block() * kBlock + threadIdx.x;
+	const int64_t tg = xcd_block() * kBlock + threadIdx.x;
+	const BatchItem it = batch_item(B, B.shadow_begin, tg);
+	const int level = it.level;
+	const int64_t t = it.local, nh = it.nh;
+	const auto& cur = *uniform_ptr(levels + level);
 	const int nl = S.n_nonambient;
 	WorkStats ws{0, 0, 0, 0};
 	const bool on = t < nh * nl;
@@ -308,8 +327,8 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
-__global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeometry fg, int level, int64_t nh,
-                                                       RayLevel cur, DeviceCounters* ctr) {
+__global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeometry fg, ShadeBatch B,
+                                                       const RayLevel* levels, DeviceCounters* ctr) {
 	// glibc pow tables in LDS: the specular pow's two dependent table lookups per light
 	// are LDS latency instead of divergent L2 gathers
 	__shared__ double log_tab[512];
@@ -317,9 +336,11 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	for (int k = threadIdx.x; k < 512; k += blockDim.x) log_tab[k] = glibc_pow_data::kLogTab[k];
 	for (int k = threadIdx.x; k < 256; k += blockDim.x) exp_tab[k] = glibc_pow_data::kExpTab[k];
 	__syncthreads();
-	const int64_t t = xcd_block() * blockDim.x + threadIdx.x;
-	if (t >= nh) return;
-	const int64_t i = cur.hit_list[t];
+	const BatchItem it = batch_item(B, B.shade_begin, xcd_block() * blockDim.x + threadIdx.x);
+	if (it.local >= it.nh) return;
+	const int level = it.level;
+	const auto& cur = *uniform_ptr(levels + level);
+	const int64_t i = cur.hit_list[it.local];
 	const int gi = cur.hgeom[i];
 	double col[3] = {0.0, 0.0, 0.0};
 	V3 o, d;
@@ -461,24 +482,25 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 	return hipGetLastError();
 }
 
-hipError_t launch_shadow(const DeviceScene& s, int level, int64_t n_hits, const RayLevel& cur, DeviceCounters* ctr,
+hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
                          unsigned long long* stats, hipStream_t stream, int packet_mask) {
-	const int64_t items = n_hits * s.n_nonambient;
-	if (items <= 0) return hipSuccess;
-	if (packet_mask & (level == 0 ? kPacketShadow0 : kPacketShadowN))
-		hipLaunchKernelGGL(k_shadow<true>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, level, n_hits, cur,
-		                   ctr, stats);
+	const int64_t items = b.shadow_begin[b.n];
+	if (items <= 0 || s.n_nonambient <= 0) return hipSuccess;
+	if (packet_mask & (b.level[0] == 0 ? kPacketShadow0 : kPacketShadowN))
+		hipLaunchKernelGGL(k_shadow<true>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, b, levels_dev, ctr,
+		                   stats);
 	else
-		hipLaunchKernelGGL(k_shadow<false>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, level, n_hits,
-		                   cur, ctr, stats);
+		hipLaunchKernelGGL(k_shadow<false>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, b, levels_dev,
+		                   ctr, stats);
 	return hipGetLastError();
 }
 
-hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n_hits, const RayLevel& cur,
+hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
                         DeviceCounters* ctr, hipStream_t stream) {
-	if (n_hits <= 0) return hipSuccess;
-	hipLaunchKernelGGL(k_shade, dim3(grid_for(n_hits, kShadeBlock)), dim3(kShadeBlock), 0, stream, s, fg, level, n_hits,
-	                   cur, ctr);
+	const int64_t items = b.shade_begin[b.n];
+	if (items <= 0) return hipSuccess;
+	hipLaunchKernelGGL(k_shade, dim3(grid_for(items, kShadeBlock)), dim3(kShadeBlock), 0, stream, s, fg, b, levels_dev,
+	                   ctr);
 	return hipGetLastError();
 }
 
