@@ -241,12 +241,13 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
 	    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) || (rc = upload(s.get(), fs.face_id, &s->ds.fid)) ||
-	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes))) {
+	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) || (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order))) {
 		rt_scene_destroy(s.release());
 		return rc;
 	}
 	s->ds.cam = fs.camera;
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
+	s->ds.n_may_raise = fs.n_may_raise;
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	s->ds.n_nonambient = 0;
 	for (size_t li = 0; li < fs.lights.size(); li++) {

@@ -25,6 +25,18 @@ struct Box {
 	}
 };
 
+// directed conversions to fp32: the result bounds x from below / above
+float round_down_f32(double x) {
+	float f = static_cast<float>(x);
+	if (static_cast<double>(f) > x) f = std::nextafter(f, -INFINITY);
+	return f;
+}
+float round_up_f32(double x) {
+	float f = static_cast<float>(x);
+	if (static_cast<double>(f) < x) f = std::nextafter(f, INFINITY);
+	return f;
+}
+
 // spread the low 21 bits of v to every third bit of a 63-bit word
 uint64_t spread3(uint64_t v) {
 	v &= 0x1fffff;
@@ -86,8 +98,8 @@ struct Builder {
 		std::memset(&n, 0, sizeof(n));
 		for (int k = 0; k < 2; k++) {
 			for (int a = 0; a < 3; a++) {
-				n.lo[k][a] = c[k].box.lo[a] - pad;
-				n.hi[k][a] = c[k].box.hi[a] + pad;
+				n.lo[k][a] = round_down_f32(c[k].box.lo[a] - pad);
+				n.hi[k][a] = round_up_f32(c[k].box.hi[a] + pad);
 			}
 			n.first[k] = c[k].first;
 			n.count[k] = c[k].count;
@@ -136,6 +148,21 @@ void world_box(const Geometry& g, const double lo[3], const double hi[3], DGeom&
 	}
 }
 
+// True unless every unit world direction is certain to keep a component above 1e-12 in
+// object space: |inv d| >= sigma_min(inv) >= |det(inv)| / ||inv||_F^2 (3x3 part).
+bool direction_may_vanish(const Affine& inv) {
+	double fro = 0;
+	for (int i = 0; i < 3; i++)
+		for (int j = 0; j < 3; j++) fro += inv.m[i][j] * inv.m[i][j];
+	const double (*m)[4] = inv.m;
+	const double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) -
+	                   m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+	                   m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+	if (!std::isfinite(fro) || !std::isfinite(det) || fro == 0) return true;
+	const double sigma_min_bound = std::fabs(det) / fro;
+	return !(sigma_min_bound > 4e-12);  // |v|_2 > sqrt(3) 1e-12 with margin for rounding
+}
+
 }  // namespace
 
 FlatScene flatten_scene(const Scene& s) {
@@ -165,6 +192,8 @@ FlatScene flatten_scene(const Scene& s) {
 		d.kind = g.kind;
 		d.flip = g.det < 0;
 		d.bvh_root = -1;
+		d.may_raise = direction_may_vanish(g.inv);
+		fs.n_may_raise += d.may_raise;
 		DMaterial m{};
 		for (int k = 0; k < 3; k++) {
 			m.ka[k] = g.mat.ka[k];
@@ -265,9 +294,13 @@ FlatScene flatten_scene(const Scene& s) {
 		std::sort(keyed.begin(), keyed.end());
 		// Conservative padding: the traversal may prune a node only when no face inside it
 		// can pass the reference's Cramer test; 1e-9 of the largest coordinate magnitude is
-		// ~10^7 ulps of slack for the slab and Cramer rounding (validated bit-exact against
-		// the oracle over every shipped scene).
-		const double pad = 1e-9 * amax + 1e-300;
+		// ~10^7 ulps of slack for the fp64 slab and Cramer rounding (validated bit-exact
+		// against the oracle over every shipped scene).  The fp32 slab test adds 2^-15 of
+		// it: rounding the ray origin o to fp32 and the fma form fma(lo, I, -fl(O*I)) move
+		// a slab plane by at most 2^-23 |o_axis| (1 + 2^-20), which this padding absorbs
+		// for |o_axis| <= 128 amax (= o_limit; intersect.h, slab32).
+		const double pad = 1e-9 * amax + 0x1p-15 * amax + 1e-300;
+		d.o_limit = 128.0 * amax;
 		const size_t node_base = fs.nodes.size();
 		for (int attempt = 0; attempt < 2; attempt++) {
 			fs.nodes.resize(node_base);
@@ -287,6 +320,15 @@ FlatScene flatten_scene(const Scene& s) {
 		d.bvh_root = static_cast<int32_t>(node_base);
 		fs.geoms.push_back(d);
 	}
+	// shadow-test order: spheres and linear meshes first, then BVH meshes by size
+	fs.shadow_order.resize(fs.geoms.size());
+	std::iota(fs.shadow_order.begin(), fs.shadow_order.end(), 0);
+	auto cost = [&](int32_t g) -> int64_t {
+		const DGeom& d = fs.geoms[g];
+		return (d.kind == GEOM_SPHERE || d.bvh_root < 0) ? 0 : d.face_count;
+	};
+	std::stable_sort(fs.shadow_order.begin(), fs.shadow_order.end(),
+	                 [&](int32_t a, int32_t b) { return cost(a) < cost(b); });
 	return fs;
 }
 

@@ -17,6 +17,10 @@ struct FlatScene {
 	std::vector<DFaceNrm> face_nrm;
 	std::vector<int32_t> face_id;
 	std::vector<DBvhNode> nodes;
+	// geometry indices in shadow-test order: the occlusion query is an `any` over the
+	// geometries, so cheap ones (spheres, linearly scanned meshes) go first
+	std::vector<int32_t> shadow_order;
+	int32_t n_may_raise = 0;
 	DCamera camera;
 	int max_bvh_depth = 0;
 };

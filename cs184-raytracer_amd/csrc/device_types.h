@@ -6,7 +6,7 @@
 //   DFaceGeo[F]     per face: p0, va = p1-p0, vb = p2-p0 (object space)      80 B
 //   DFaceNrm[F]     per face: n0, n1, n2 (object space, w == 0 dropped)       80 B
 //   int32 face_id[F]  face index within its mesh in the reference's order (tie-break)
-//   DBvhNode[N]     flattened binary LBVH, child boxes stored in the parent   128 B
+//   DBvhNode[N]     flattened binary LBVH, fp32 child boxes stored in the parent  64 B
 // BVH meshes store their faces in LBVH leaf order; small meshes (<= kLinearFaces) keep
 // the reference's order and are scanned linearly exactly like geometry.cpp:78.
 #pragma once
@@ -34,7 +34,15 @@ struct alignas(16) DGeom {
 	int32_t bvh_root;     // root node index, -1 = linear face scan
 	int32_t face_begin, face_count;
 	int32_t mat;          // index into DMaterial
-	int32_t pad;
+	// The inverse transform may map a unit direction to one the reference rejects as
+	// "ray has no direction" (rtbase.h:17-23): every ray must then check this geometry,
+	// even where culling or an early exit would skip it (bvh.cpp, intersect.h).
+	int32_t may_raise;
+	// The fp32 node slab test is conservative for object-space ray origins with every
+	// |coordinate| <= o_limit (the node boxes carry the padding for that); rays from
+	// farther away use the fp64 slab test on the same boxes (intersect.h).
+	double o_limit;
+	double pad2;
 };
 
 struct alignas(16) DMaterial {   // rtbase.h:30-39
@@ -63,13 +71,13 @@ struct alignas(16) DFaceNrm {
 };
 
 // child c of a node: leaf when count[c] > 0 (faces [first[c], first[c]+count[c])),
-// else inner node index first[c].  Boxes are padded outward (see bvh.cpp).
-struct alignas(16) DBvhNode {
-	double lo[2][3];
-	double hi[2][3];
+// else inner node index first[c].  Boxes are padded outward and rounded outward to fp32
+// (see bvh.cpp): one node is one 64-B half cache line.
+struct alignas(64) DBvhNode {
+	float lo[2][3];
+	float hi[2][3];
 	int32_t first[2];
 	int32_t count[2];
-	double pad[2];
 };
 
 struct DCamera {

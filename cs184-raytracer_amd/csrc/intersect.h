@@ -213,6 +213,71 @@ __device__ __forceinline__ V3 safe_inv(V3 d) {
 
 __device__ __forceinline__ double prune_limit(double best_dist) { return best_dist * (1.0 + 4e-9); }
 
+// ---------------------------------------------------------------- fp32 node slab test
+// Conservative fp32 form of slab() for the fp32 node boxes (bvh.cpp): with O = fl32(o),
+// I = fl32(fl64(1/d)) and t = fma(lo, I, -fl32(O * I)), each computed plane distance is
+// the exact distance to a plane moved by at most 2^-23 |o_axis| (absorbed by the box
+// padding while |o_axis| <= o_limit), times a factor within 1 +- 2^-22 (absorbed by the
+// relative widening 2^-20).  |I| is clamped to 2^60: for a direction component below
+// 2^-60 the clamped distances to the padded planes still exceed any face distance.
+// No NaN can arise except from widening an infinite entry/exit, which is a true miss.
+struct Ray32 {
+	float ix, iy, iz;     // I
+	float oix, oiy, oiz;  // fl32(O * I)
+};
+__device__ __forceinline__ float clamp_inv(double inv) {
+	return fminf(fmaxf(static_cast<float>(inv), -0x1p60f), 0x1p60f);
+}
+__device__ __forceinline__ Ray32 ray32(V3 o, V3 inv) {
+	Ray32 r;
+	r.ix = clamp_inv(inv.x);
+	r.iy = clamp_inv(inv.y);
+	r.iz = clamp_inv(inv.z);
+	r.oix = static_cast<float>(o.x) * r.ix;
+	r.oiy = static_cast<float>(o.y) * r.iy;
+	r.oiz = static_cast<float>(o.z) * r.iz;
+	return r;
+}
+// the fp32 slab test is valid for this object-space origin (bvh.cpp, o_limit)
+#ifndef RT_NODE_F32
+#define RT_NODE_F32 0
+#endif
+__device__ __forceinline__ bool origin_fits_f32(V3 o, double o_limit) {
+	if (!RT_NODE_F32) return false;
+	return fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) <= o_limit;
+}
+// lim rounded up to fp32
+__device__ __forceinline__ float limit_f32(double lim) {
+	float f = static_cast<float>(lim);
+	if (static_cast<double>(f) < lim)  // next float up (f is finite here)
+		f = f == 0.0f ? 0x1p-149f : __uint_as_float(__float_as_uint(f) + (f > 0.0f ? 1u : 0xffffffffu));
+	return f;
+}
+template <typename P>
+__device__ __forceinline__ bool slab32(P lo, P hi, const Ray32& r, float lim, float& tnear) {
+	const float tx0 = fmaf(lo[0], r.ix, -r.oix), tx1 = fmaf(hi[0], r.ix, -r.oix);
+	const float ty0 = fmaf(lo[1], r.iy, -r.oiy), ty1 = fmaf(hi[1], r.iy, -r.oiy);
+	const float tz0 = fmaf(lo[2], r.iz, -r.oiz), tz1 = fmaf(hi[2], r.iz, -r.oiz);
+	float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+	float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+	tmin = fmaf(-fabsf(tmin), 0x1p-20f, tmin);
+	tmax = fmaf(fabsf(tmax), 0x1p-20f, tmax);
+	tnear = tmin;
+	return tmax >= tmin && tmax >= 0.0f && tmin <= lim;
+}
+// one child box of a node: fp32 test, or fp64 on the same boxes for far origins
+template <typename P>
+__device__ __forceinline__ bool node_slab(P lo, P hi, bool f32, const Ray32& r, float lim32, V3 o, V3 inv, double lim,
+                                          double& tnear) {
+	if (f32) {
+		float t;
+		const bool h = slab32(lo, hi, r, lim32, t);
+		tnear = t;
+		return h;
+	}
+	return slab(lo, hi, o, inv, lim, tnear);
+}
+
 // Mesh::calculateIntNormInObjSpace (geometry.cpp:69-126) with an LBVH in place of the
 // linear scan for large meshes.
 //   kAnyHit = false: the reference's closest face (returns found, Po, No).
@@ -247,6 +312,8 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 		// child's entry distance (rounded down to float) so that a popped subtree the
 		// search has since pruned (it begins beyond the best face) is skipped.
 		const V3 inv = safe_inv(d);
+		const Ray32 r32 = ray32(o, inv);
+		const bool f32 = origin_fits_f32(o, G->o_limit);
 		float* tstack = reinterpret_cast<float*>(stack + kStackDepth * kBlock);
 		(void)tstack;
 		int32_t ref = G->bvh_root;
@@ -269,8 +336,9 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 				const DBvhNode* N = S.nodes + ref;
 				double tn0, tn1;
 				const double lim = fmin(prune_limit(best.dist), prune_cap);
-				const bool h0 = slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
-				const bool h1 = slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+				const float lim32 = limit_f32(lim);
+				const bool h0 = node_slab(N->lo[0], N->hi[0], f32, r32, lim32, o, inv, lim, tn0);
+				const bool h1 = node_slab(N->lo[1], N->hi[1], f32, r32, lim32, o, inv, lim, tn1);
 				if (h0 || h1) {
 					const int c = (h0 && h1) ? (tn1 < tn0 ? 1 : 0) : (h1 ? 1 : 0);
 					const int32_t cf = N->first[c], cc = N->count[c];
@@ -305,6 +373,8 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 	}
 #else
 		const V3 inv = safe_inv(d);
+		const Ray32 r32 = ray32(o, inv);
+		const bool f32 = origin_fits_f32(o, G->o_limit);
 		int32_t node = G->bvh_root;
 		int sp = 0;
 		for (;;) {
@@ -312,8 +382,9 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 			const DBvhNode* N = S.nodes + node;
 			double tn0, tn1;
 			const double lim = fmin(prune_limit(best.dist), prune_cap);
-			const bool h0 = slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
-			const bool h1 = slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+			const float lim32 = limit_f32(lim);
+			const bool h0 = node_slab(N->lo[0], N->hi[0], f32, r32, lim32, o, inv, lim, tn0);
+			const bool h1 = node_slab(N->lo[1], N->hi[1], f32, r32, lim32, o, inv, lim, tn1);
 			const int first = (h0 && h1 && tn1 < tn0) ? 1 : 0;
 			int32_t next = -1;
 #pragma unroll
@@ -373,6 +444,18 @@ __device__ __forceinline__ bool sphere_hit(GP G, V3 o, V3 d, bool reverse, V3& P
 	return true;
 }
 
+// Every castRay transforms the ray into every geometry's object space, which throws for
+// a vanishing direction (geometry.cpp:33, rtbase.h:17-23).  Culling and early exits skip
+// geometries, so those whose transform can make a direction vanish (DGeom::may_raise,
+// bvh.cpp) are checked here for every ray; for all others the check cannot fire.
+__device__ __forceinline__ void check_may_raise(const DeviceScene& S, V3 d, bool on, DeviceCounters* ctr) {
+	if (S.n_may_raise == 0) return;
+	for (int g = 0; g < S.n_geoms; g++) {
+		const auto G = uniform_ptr(S.geoms) + g;
+		if (G->may_raise && on && is_zero3(xf_dir(G->inv, d))) raise_error(ctr, DERR_NO_DIRECTION);
+	}
+}
+
 // Closest hit of Scene::castRay (scene.cpp:142-167): world distance, strict `<` in
 // insertion order.  A geometry whose padded world box the ray misses, or enters beyond
 // the current best distance, cannot be the answer and is skipped without its
@@ -381,6 +464,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
                             V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WorkStats& ws) {
 	bool found = false;
 	const V3 winv = safe_inv(d);
+	check_may_raise(S, d, true, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
@@ -420,7 +504,10 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
                          DeviceCounters* ctr, WorkStats& ws) {
 	const V3 winv = safe_inv(d);
 	const bool inf_light = dist_light == INFINITY;
-	for (int g = 0; g < S.n_geoms; g++) {
+	check_may_raise(S, d, true, ctr);
+	// `any` over the geometries: cheap ones first (DeviceScene::shadow_order)
+	for (int k = 0; k < S.n_geoms; k++) {
+		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
 		if (!slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw)) continue;
@@ -492,6 +579,8 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				}
 		} else {
 			const V3 inv = safe_inv(d);
+			const Ray32 r32 = ray32(o, inv);
+			const bool f32 = origin_fits_f32(o, G->o_limit);
 			const auto nodes = uniform_ptr(S.nodes);
 			int32_t node = G->bvh_root;
 			int sp = 0;
@@ -500,8 +589,9 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				if (live) ws.nodes++;
 				double tn0 = 0, tn1 = 0;
 				const double lim = fmin(prune_limit(best.dist), prune_cap);
-				const bool h0 = live && slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
-				const bool h1 = live && slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+				const float lim32 = limit_f32(lim);
+				const bool h0 = live && node_slab(N->lo[0], N->hi[0], f32, r32, lim32, o, inv, lim, tn0);
+				const bool h1 = live && node_slab(N->lo[1], N->hi[1], f32, r32, lim32, o, inv, lim, tn1);
 				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
 				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
 				const int first = (2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0;
@@ -550,6 +640,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
                                    WorkStats& ws) {
 	bool found = false;
 	const V3 winv = safe_inv(d);
+	check_may_raise(S, d, on, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
@@ -589,7 +680,9 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 	const V3 winv = safe_inv(d);
 	const bool inf_light = dist_light == INFINITY;
 	bool occ = false;
-	for (int g = 0; g < S.n_geoms; g++) {
+	check_may_raise(S, d, on, ctr);
+	for (int k = 0; k < S.n_geoms; k++) {
+		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
 		const bool cand = on && !occ && slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);

@@ -16,8 +16,10 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DFaceNrm* fnrm;
 	const int32_t* fid;
 	const DBvhNode* nodes;
+	const int32_t* shadow_order;              // geometry order of the occlusion query
 	DCamera cam;
 	int32_t n_geoms, n_lights, n_nonambient;
+	int32_t n_may_raise;                      // geometries with DGeom::may_raise
 	int32_t occl_stride;                      // bytes per ray in RayLevel::occl (n_nonambient rounded to 8)
 	int32_t shadow_light[kMaxShadowLights];  // j-th non-ambient light -> light index
 };
