@@ -24,8 +24,13 @@ sys.path.insert(0, os.path.join(REPO, "cs184-raytracer_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
-NODE_BYTES, TRI_BYTES, NRM_BYTES = 128, 72, 72   # SURVEY.md §8d algorithmic bytes
+NODE_BYTES, TRI_BYTES, NRM_BYTES = 64, 72, 72   # SURVEY.md §8d algorithmic bytes (64-B fp32-box node)
 RAY_IO_BYTES, PIXEL_BYTES = 64 + 64, 24
+FP64_PEAK_TFLOPS = 78.6     # MI355X vector FP64
+# algorithmic fp64 flops: node visit = two 28-flop slab tests; a triangle
+# test 38 flops to the a-reject, +67 for one that reaches the normal + facing test; a
+# sphere test 30 + two 28-flop transforms + 12 for the re-normalisation
+NODE_FLOPS, TRI_FLOPS, CAND_FLOPS, SPHERE_FLOPS = 56, 38, 67, 98
 
 
 def parse():
@@ -116,7 +121,8 @@ def main():
     frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     from rtamd import dist as rd
 
-    totals = {"rays": 0, "ms": [0.0, 0.0, 0.0], "launches": [0, 0, 0], "bytes": [0, 0, 0]}
+    totals = {"rays": 0, "trace_rays": 0, "ms": [0.0, 0.0, 0.0], "launches": [0, 0, 0], "bytes": [0, 0, 0],
+              "flops": [0, 0, 0]}
     work = {}
 
     def step(record):
@@ -125,6 +131,7 @@ def main():
             rd.gather_rows(out8, H, dst=0, out=frame, bufs=gather)  # RCCL gather of RGB8 rows
             if record:
                 totals["rays"] += st.trace_rays + st.shadow_rays
+                totals["trace_rays"] += st.trace_rays
                 for k in range(3):
                     totals["ms"][k] += st.stage_ms[k]
                     totals["launches"][k] += st.stage_launches[k]
@@ -132,6 +139,8 @@ def main():
                 for k, nrays in ((0, st.trace_rays), (1, st.shadow_rays)):
                     totals["bytes"][k] += (nrays * RAY_IO_BYTES + st.stage_node_visits[k] * NODE_BYTES +
                                            st.stage_tri_tests[k] * TRI_BYTES + st.stage_candidates[k] * NRM_BYTES)
+                    totals["flops"][k] += (st.stage_node_visits[k] * NODE_FLOPS + st.stage_tri_tests[k] * TRI_FLOPS +
+                                           st.stage_candidates[k] * CAND_FLOPS + st.stage_sphere_tests[k] * SPHERE_FLOPS)
                 totals["bytes"][2] += st.pixels * PIXEL_BYTES
                 work.update({"trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
                              "node_visits": list(st.stage_node_visits), "tri_tests": list(st.stage_tri_tests),
@@ -150,7 +159,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     agg = torch.tensor([elapsed, float(totals["rays"])] + totals["ms"] + [float(x) for x in totals["launches"]] +
-                       [float(x) for x in totals["bytes"]], dtype=torch.float64, device="cuda")
+                       [float(x) for x in totals["bytes"]] + [float(x) for x in totals["flops"]] +
+                       [float(totals["trace_rays"])], dtype=torch.float64, device="cuda")
     if world > 1:
         t_max = agg[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -158,12 +168,14 @@ def main():
         agg[0] = t_max[0]
     v = agg.tolist()
     elapsed, rays, stage_ms, stage_launches, stage_bytes = v[0], v[1], v[2:5], v[5:8], v[8:11]
+    stage_flops, trace_rays = v[11:14], v[14]
     if rank == 0:
         value = rays / elapsed / 1e6
         names = ["k_closest", "k_shadow", "k_shade"]
         dom = max(range(3), key=lambda k: stage_ms[k])  # the dominant kernel
         kms, launches, nbytes = stage_ms[dom], stage_launches[dom], stage_bytes[dom]
         achieved = (nbytes / launches) / ((kms / launches) * 1e-3) / 1e9 if launches else 0.0
+        gflops = stage_flops[dom] / (kms * 1e-3) / 1e9 if kms else 0.0
         traffic = None
         if os.path.exists(a.traffic):
             try:
@@ -174,6 +186,7 @@ def main():
             "metric": "Mrays/s (primary+secondary) and wall-clock at 1920x1080; HBM GB/s vs peak",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "mrays_trace": round(trace_rays / elapsed / 1e6, 3),
             "vs_baseline": None, "dtype": "f64", "data": "synthetic: shipped reference scene data (bunny.obj), "
                                                         "deterministic, no RNG",
             "config": {"workload": a.config, "scene": scene_rel, "width": W, "height": H,
@@ -183,8 +196,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": names[dom], "avg_launch_ms": round(kms / launches, 4) if launches else None,
+                         "fp64": {"achieved": round(gflops / 1e3, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                  "frac": round(gflops / 1e3 / FP64_PEAK_TFLOPS, 4)},
                          "note": "algorithmic bytes per SURVEY.md §8d (ray I/O + LBVH nodes + triangles + normals), "
-                                 "mostly L2-resident scene reads; see DESIGN.md",
+                                 "mostly L2/MALL-resident scene reads; kernel times are HIP-event spans of launches "
+                                 "that run concurrently with other levels' kernels; see DESIGN.md",
                          "stages": {names[k]: {"ms_per_frame": round(stage_ms[k] / a.steps / world, 4),
                                                "launches_per_frame": stage_launches[k] / a.steps / world,
                                                "GBps": round(stage_bytes[k] / (stage_ms[k] * 1e-3) / 1e9, 1)

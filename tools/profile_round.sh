@@ -9,10 +9,10 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
-cd $R
-timeout -k 10 300 python bench.py --steps 10 --warmup 2 > $O/bench.json 2> $O/bench.err || exit 1
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/kt.log 2>&1 || exit 2
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o pmc --output-format csv -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/fetch.log 2>&1 || exit 3
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o pmc --output-format csv -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/write.log 2>&1 || exit 4
+cd $R
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > $O/bench.json 2> $O/bench.err || exit 1
 echo done
