@@ -144,7 +144,8 @@ def main():
                 totals["bytes"][2] += st.pixels * PIXEL_BYTES
                 work.update({"trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
                              "node_visits": list(st.stage_node_visits), "tri_tests": list(st.stage_tri_tests),
-                             "candidates": list(st.stage_candidates), "sphere_tests": list(st.stage_sphere_tests)})
+                             "candidates": list(st.stage_candidates), "sphere_tests": list(st.stage_sphere_tests),
+                             "bvh_traversals": list(st.stage_bvh_traversals)})
 
     for _ in range(a.warmup):
         step(False)

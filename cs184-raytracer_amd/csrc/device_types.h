@@ -18,7 +18,10 @@ enum : int32_t { DGEOM_SPHERE = 0, DGEOM_MESH = 1 };
 enum : int32_t { DLIGHT_POINT = 0, DLIGHT_DIRECTIONAL = 1, DLIGHT_AMBIENT = 2 };
 
 constexpr int kLinearFaces = 8;   // meshes up to this size are scanned linearly (no BVH)
-constexpr int kLeafFaces = 4;     // faces per LBVH leaf
+#ifndef RT_LEAF_FACES
+#define RT_LEAF_FACES 4
+#endif
+constexpr int kLeafFaces = RT_LEAF_FACES;  // faces per LBVH leaf
 constexpr int kStackDepth = 32;   // traversal stack entries per lane (LDS); LBVH depth <= 30
 
 struct alignas(16) DGeom {

@@ -122,7 +122,7 @@ __device__ bool hits_bounding_box(V3 o, V3 d, P mn, P mx) {
 
 // Per-lane work counters (algorithmic bytes/flops of the roofline)
 struct WorkStats {
-	uint32_t nodes, tris, cands, spheres;
+	uint32_t nodes, tris, cands, spheres, bvh_entries;
 };
 
 struct MeshBest {
@@ -311,6 +311,7 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 		// <= -2 a leaf (face offset << 3 | count), -1 done.  The stack keeps each far
 		// child's entry distance (rounded down to float) so that a popped subtree the
 		// search has since pruned (it begins beyond the best face) is skipped.
+		ws.bvh_entries++;
 		const V3 inv = safe_inv(d);
 		const Ray32 r32 = ray32(o, inv);
 		const bool f32 = origin_fits_f32(o, G->o_limit);
@@ -578,6 +579,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					live = false;
 				}
 		} else {
+			if (live) ws.bvh_entries++;
 			const V3 inv = safe_inv(d);
 			const Ray32 r32 = ray32(o, inv);
 			const bool f32 = origin_fits_f32(o, G->o_limit);

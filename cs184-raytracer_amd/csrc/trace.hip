@@ -101,15 +101,17 @@ __device__ __forceinline__ unsigned long long* shard(unsigned long long* stats) 
 }
 
 __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long long* stats, int stage) {
-	unsigned long long w4[4] = {ws.nodes, ws.tris, ws.cands, ws.spheres};
+	unsigned long long w[5] = {ws.nodes, ws.tris, ws.cands, ws.spheres, ws.bvh_entries};
 #pragma unroll
-	for (int k = 0; k < 4; k++)
-		for (int o = 32; o > 0; o >>= 1) w4[k] += __shfl_xor(w4[k], o);
+	for (int k = 0; k < 5; k++)
+		for (int o = 32; o > 0; o >>= 1) w[k] += __shfl_xor(w[k], o);
 	if (__lane_id() == 0) {
-		unsigned long long* sh = shard(stats) + (stage ? ST_NODES1 : ST_NODES0);
+		unsigned long long* sh = shard(stats);
+		const int base = stage ? ST_NODES1 : ST_NODES0;
 #pragma unroll
 		for (int k = 0; k < 4; k++)
-			if (w4[k]) atomicAdd(sh + k, w4[k]);
+			if (w[k]) atomicAdd(sh + base + k, w[k]);
+		if (w[4]) atomicAdd(sh + (stage ? ST_ENTRIES1 : ST_ENTRIES0), w[4]);
 	}
 }
 
@@ -162,7 +164,7 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScen
 	const int64_t t = xcd_block() * kBlock + threadIdx.x;
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
-	WorkStats ws{0, 0, 0, 0};
+	WorkStats ws{0, 0, 0, 0, 0};
 	bool hit = false;
 	int gi = -1;
 	double dist = 0;
@@ -297,7 +299,7 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene
 	const int64_t t = it.local, nh = it.nh;
 	const auto& cur = *uniform_ptr(levels + level);
 	const int nl = S.n_nonambient;
-	WorkStats ws{0, 0, 0, 0};
+	WorkStats ws{0, 0, 0, 0, 0};
 	const bool on = t < nh * nl;
 	int32_t i = 0;
 	int j = 0;

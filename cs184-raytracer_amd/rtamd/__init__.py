@@ -65,7 +65,7 @@ class rt_counters(ctypes.Structure):
                 ("sphere_tests", ctypes.c_int64), ("stage_ms", ctypes.c_double * 3),
                 ("stage_launches", ctypes.c_int32 * 3), ("stage_node_visits", ctypes.c_int64 * 2),
                 ("stage_tri_tests", ctypes.c_int64 * 2), ("stage_candidates", ctypes.c_int64 * 2),
-                ("stage_sphere_tests", ctypes.c_int64 * 2)]
+                ("stage_sphere_tests", ctypes.c_int64 * 2), ("stage_bvh_traversals", ctypes.c_int64 * 2)]
 
 
 class rt_scene_info(ctypes.Structure):
@@ -167,6 +167,7 @@ class RenderStats:
     stage_tri_tests: tuple = ()
     stage_candidates: tuple = ()
     stage_sphere_tests: tuple = ()
+    stage_bvh_traversals: tuple = ()
 
     @property
     def rays(self) -> int:
@@ -178,7 +179,8 @@ def _stats(c: rt_counters) -> RenderStats:
     return RenderStats(c.trace_rays, c.shadow_rays, c.reflect_rays, c.refract_rays, c.pixels, c.intersection_max,
                        c.kernel_ms, c.levels, c.trace_launches, c.node_visits, c.tri_tests, c.candidates,
                        c.sphere_tests, tuple(c.stage_ms), tuple(c.stage_launches), tuple(c.stage_node_visits),
-                       tuple(c.stage_tri_tests), tuple(c.stage_candidates), tuple(c.stage_sphere_tests))
+                       tuple(c.stage_tri_tests), tuple(c.stage_candidates), tuple(c.stage_sphere_tests),
+                       tuple(c.stage_bvh_traversals))
 
 
 class Scene:
