@@ -6,6 +6,12 @@
 #include <numeric>
 #include "xform.h"
 
+// Tree construction: binned SAH (1) or Morton radix splits (0); any tree gives the same
+// results (intersect.h), the choice only moves traversal cost.
+#ifndef RT_BVH_SAH
+#define RT_BVH_SAH 1
+#endif
+
 namespace rtamd {
 namespace {
 
@@ -57,6 +63,7 @@ struct Builder {
 	double pad;
 	int max_depth = 0;
 	bool median_only = false;
+	bool sah = true;
 
 	struct Ref {
 		Box box;
@@ -77,6 +84,69 @@ struct Builder {
 		return lo + 1;
 	}
 
+	static double area(const Box& x) {
+		const double dx = x.hi[0] - x.lo[0], dy = x.hi[1] - x.lo[1], dz = x.hi[2] - x.lo[2];
+		return dx * dy + dy * dz + dz * dx;
+	}
+
+	// Binned surface-area-heuristic split of order[b, e) (reorders it in place): the split
+	// between centroid bins minimising area(L) * |L| + area(R) * |R| over the three axes.
+	int sah_split(int b, int e) {
+		constexpr int kBins = 32;
+		double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+		auto centre = [&](int32_t f, int a) { return 0.5 * (boxes[f].lo[a] + boxes[f].hi[a]); };
+		for (int i = b; i < e; i++)
+			for (int a = 0; a < 3; a++) {
+				clo[a] = std::min(clo[a], centre(order[i], a));
+				chi[a] = std::max(chi[a], centre(order[i], a));
+			}
+		double best = INFINITY;
+		int best_axis = -1, best_bin = -1;
+		for (int a = 0; a < 3; a++) {
+			const double ext = chi[a] - clo[a];
+			if (!(ext > 0)) continue;
+			Box bb[kBins];
+			int cnt[kBins] = {0};
+			for (auto& x : bb) x.empty();
+			for (int i = b; i < e; i++) {
+				const int k = std::min(kBins - 1, static_cast<int>((centre(order[i], a) - clo[a]) / ext * kBins));
+				cnt[k]++;
+				bb[k].grow(boxes[order[i]]);
+			}
+			double right_area[kBins];
+			int right_cnt[kBins];
+			Box acc;
+			acc.empty();
+			int n = 0;
+			for (int k = kBins - 1; k > 0; k--) {
+				acc.grow(bb[k]);
+				n += cnt[k];
+				right_area[k] = area(acc);
+				right_cnt[k] = n;
+			}
+			acc.empty();
+			n = 0;
+			for (int k = 0; k < kBins - 1; k++) {
+				acc.grow(bb[k]);
+				n += cnt[k];
+				if (n == 0 || right_cnt[k + 1] == 0) continue;
+				const double c = area(acc) * n + right_area[k + 1] * right_cnt[k + 1];
+				if (c < best) {
+					best = c;
+					best_axis = a;
+					best_bin = k;
+				}
+			}
+		}
+		if (best_axis < 0) return (b + e) / 2;  // all centroids coincide
+		const double ext = chi[best_axis] - clo[best_axis];
+		auto* mid = std::partition(order.data() + b, order.data() + e, [&](int32_t f) {
+			return std::min(kBins - 1, static_cast<int>((centre(f, best_axis) - clo[best_axis]) / ext * kBins)) <= best_bin;
+		});
+		const int m = static_cast<int>(mid - order.data());
+		return (m == b || m == e) ? (b + e) / 2 : m;
+	}
+
 	Ref build(int b, int e, int depth) {
 		max_depth = std::max(max_depth, depth);
 		Ref r;
@@ -92,7 +162,7 @@ struct Builder {
 		}
 		const int idx = static_cast<int>(nodes.size());
 		nodes.emplace_back();
-		const int m = split(b, e);
+		const int m = (sah && !median_only) ? sah_split(b, e) : split(b, e);
 		const Ref c[2] = {build(b, m, depth + 1), build(m, e, depth + 1)};
 		DBvhNode& n = nodes[idx];
 		std::memset(&n, 0, sizeof(n));
@@ -306,6 +376,7 @@ FlatScene flatten_scene(const Scene& s) {
 			fs.nodes.resize(node_base);
 			Builder bld{boxes, {}, {}, fs.nodes, {}, pad};
 			bld.median_only = attempt == 1;
+			bld.sah = RT_BVH_SAH;
 			for (const auto& kv : keyed) {
 				bld.code.push_back(kv.first);
 				bld.order.push_back(kv.second);
