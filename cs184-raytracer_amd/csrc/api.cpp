@@ -46,40 +46,60 @@ struct rt_builder {
 	rtamd::Scene scene;
 };
 
+
 struct LevelBuffers {
 	rtamd::RayLevel lv{};
 	void* block = nullptr;
 };
 
+// One render pipeline: its own level buffers, streams and events, tracing one chunk of
+// rows at a time.  A frame is split into chunks that several lanes trace concurrently:
+// every level of a chunk waits for the previous one (and the host reads its counts), so
+// a single chain leaves the GPU idle in its small deep levels; other lanes' chunks fill
+// those gaps (tools/tail_test.py: 1/8 of the C3 frame alone takes 55 % of the frame's time).
+struct Lane {
+	hipStream_t stream = nullptr;        // k_closest chain, reduce, output (high priority)
+	// k_shadow + k_shade of level L < direct_levels on shade[L % 3]; the small deep levels
+	// are shaded in batches on shade[3] once the chain has finished
+	hipStream_t shade[4] = {nullptr, nullptr, nullptr, nullptr};
+	std::vector<LevelBuffers> levels;
+	// RayLevel records of all levels for the batched shading kernels (pinned + device)
+	rtamd::RayLevel* levels_pinned = nullptr;
+	rtamd::RayLevel* levels_dev = nullptr;
+	size_t levels_cap = 0;
+	// per level: [0] before k_closest, [1] after it (the shading streams wait on it);
+	// per shading launch, in the events of its first level: [2] before k_shadow, [3] after
+	// it, [4] after k_shade (the reduce waits on it)
+	std::vector<std::array<hipEvent_t, 5>> level_events;
+	hipEvent_t counts_ready = nullptr;   // level counts copied to counts_host
+	hipEvent_t chunk_done = nullptr;     // output of the chunk written
+	int32_t* counts_host = nullptr;      // pinned: hits, children, error word
+	// chunk state
+	enum Phase { IDLE, TRACING, FINISHING } phase = IDLE;
+	rtamd::FrameGeometry fg{};
+	int64_t r0 = 0, n0 = 0;
+	int level = 0;
+	std::vector<int64_t> level_n;
+	std::vector<int> shaded;                        // first level of each shading launch
+	std::vector<std::pair<int, int64_t>> deferred;  // (level, hits) shaded after the chain
+};
+
 struct rt_scene {
 	int device = 0;
-	hipStream_t stream = nullptr;
+	hipStream_t stream = nullptr;                // default caller stream (rt_render, normalize)
 	rtamd::DeviceScene ds{};
 	std::vector<void*> allocs;
 	rt_scene_info info{};
-	std::vector<LevelBuffers> levels;
+	std::vector<std::unique_ptr<Lane>> lanes;
 	rtamd::DeviceCounters* ctr = nullptr;        // device
 	rtamd::DeviceCounters* ctr_host = nullptr;   // pinned mirror
 	unsigned long long* stats = nullptr;         // device, kStatShards x kStatStride
 	std::vector<unsigned long long> stats_host;
 	double* out_dev = nullptr;                   // staging for rt_render
 	int64_t out_capacity = 0;
-	// Shading streams: k_shadow + k_shade of level L < direct_levels run on
-	// shade_streams[L % 3] while the render stream (high priority: it carries the critical
-	// path) traces level L+1; the deeper, smaller levels are shaded together in batches on
-	// shade_streams[3] once the closest-hit chain has finished.
-	hipStream_t shade_streams[4] = {nullptr, nullptr, nullptr, nullptr};
+	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
 	int direct_levels = 3;
-	// RayLevel records of all levels for the batched shading kernels (pinned + device)
-	rtamd::RayLevel* levels_pinned = nullptr;
-	rtamd::RayLevel* levels_dev = nullptr;
-	size_t levels_cap = 0;
-	hipEvent_t fork_event = nullptr;             // caller's stream -> render stream
-	// per level: [0] before k_closest, [1] after it (the shading streams wait on it);
-	// per shading launch, in the events of its first level: [2] before k_shadow, [3] after
-	// it, [4] after k_shade (the reduce waits on it)
-	std::vector<std::array<hipEvent_t, 5>> level_events;
-	int32_t* counts_host = nullptr;              // pinned: level counts + error word
+	int chunks_per_lane = 2;
 	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketShadow0;  // measured best on C3
 };
 
@@ -99,10 +119,10 @@ int upload(rt_scene* s, const std::vector<T>& host, const T** dev) {
 }
 
 // Level buffers grow on demand and are kept for later renders (HBM is plentiful:
-// ~105 B per ray record).
-int ensure_level(rt_scene* s, size_t level, int64_t capacity) {
-	if (s->levels.size() <= level) s->levels.resize(level + 1);
-	LevelBuffers& L = s->levels[level];
+// ~130 B per ray record).
+int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
+	if (ln.levels.size() <= level) ln.levels.resize(level + 1);
+	LevelBuffers& L = ln.levels[level];
 	if (L.lv.capacity >= capacity) return RT_OK;
 	if (L.block) {
 		HIP_TRY(hipDeviceSynchronize());
@@ -139,36 +159,209 @@ int ensure_level(rt_scene* s, size_t level, int64_t capacity) {
 
 // Level `level` exists and its RayLevel record is in the pinned array (the record of an
 // earlier level never changes while copies of it may be in flight).
-int ensure_level_record(rt_scene* s, size_t level, int64_t capacity) {
-	if (level + 1 > s->levels_cap) {
+int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
+	if (level + 1 > ln.levels_cap) {
 		HIP_TRY(hipDeviceSynchronize());
 		const size_t cap = std::max<size_t>(16, 2 * (level + 1));
 		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
 		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), hipHostMallocDefault));
 		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dev), cap * sizeof(rtamd::RayLevel)));
-		if (s->levels_pinned) {
-			std::memcpy(pin, s->levels_pinned, s->levels_cap * sizeof(rtamd::RayLevel));
-			(void)hipHostFree(s->levels_pinned);
-			(void)hipFree(s->levels_dev);
+		if (ln.levels_pinned) {
+			std::memcpy(pin, ln.levels_pinned, ln.levels_cap * sizeof(rtamd::RayLevel));
+			(void)hipHostFree(ln.levels_pinned);
+			(void)hipFree(ln.levels_dev);
 		}
-		s->levels_pinned = pin;
-		s->levels_dev = dev;
-		s->levels_cap = cap;
+		ln.levels_pinned = pin;
+		ln.levels_dev = dev;
+		ln.levels_cap = cap;
 	}
-	int rc = ensure_level(s, level, capacity);
+	int rc = ensure_level(s, ln, level, capacity);
 	if (rc) return rc;
-	s->levels_pinned[level] = s->levels[level].lv;
+	ln.levels_pinned[level] = ln.levels[level].lv;
 	return RT_OK;
 }
 
-int ensure_events(rt_scene* s, size_t level) {
-	while (s->level_events.size() <= level) {
+int ensure_events(Lane& ln, size_t level) {
+	while (ln.level_events.size() <= level) {
 		std::array<hipEvent_t, 5> ev{};
 		for (hipEvent_t& e : ev) HIP_TRY(hipEventCreate(&e));
-		s->level_events.push_back(ev);
+		ln.level_events.push_back(ev);
 	}
 	return RT_OK;
 }
+
+int lane_create(Lane& ln, int prio_low, int prio_high) {
+	HIP_TRY(hipStreamCreateWithPriority(&ln.stream, hipStreamNonBlocking, prio_high));
+	for (hipStream_t& q : ln.shade) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
+	HIP_TRY(hipEventCreateWithFlags(&ln.counts_ready, hipEventDisableTiming));
+	HIP_TRY(hipEventCreateWithFlags(&ln.chunk_done, hipEventDisableTiming));
+	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.counts_host), 4 * sizeof(int32_t), hipHostMallocDefault));
+	return RT_OK;
+}
+
+void lane_destroy(Lane& ln) {
+	for (auto& L : ln.levels)
+		if (L.block) (void)hipFree(L.block);
+	if (ln.levels_pinned) (void)hipHostFree(ln.levels_pinned);
+	if (ln.levels_dev) (void)hipFree(ln.levels_dev);
+	if (ln.counts_host) (void)hipHostFree(ln.counts_host);
+	for (auto& ev : ln.level_events)
+		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+	if (ln.counts_ready) (void)hipEventDestroy(ln.counts_ready);
+	if (ln.chunk_done) (void)hipEventDestroy(ln.chunk_done);
+	for (hipStream_t q : ln.shade)
+		if (q) (void)hipStreamDestroy(q);
+	if (ln.stream) (void)hipStreamDestroy(ln.stream);
+}
+
+// The render of one rt_render_device call: chunks of rows handed to lanes, each lane a
+// small state machine advanced by the host as its events complete.
+struct Render {
+	rt_scene* s;
+	int depth, io;
+	double* out_rgb_dev;
+	uint8_t* out_rgb8_dev;
+	int64_t W;
+	rt_counters cnt{};
+	float kernel_ms = 0.f;
+
+	// k_closest of the lane's current level, then the counts read-back
+	int launch_level(Lane& ln) {
+		const int L = ln.level;
+		const int remaining = depth - L;
+		const int64_t n = ln.level_n[L];
+		int rc;
+		if (remaining > 0 && (rc = ensure_level_record(s, ln, L + 1, 2 * n))) return rc;
+		if ((rc = ensure_events(ln, L))) return rc;
+		const auto& ev = ln.level_events[L];
+		const rtamd::RayLevel& cur = ln.levels[L].lv;
+		const rtamd::RayLevel& next = remaining > 0 ? ln.levels[L + 1].lv : cur;
+		HIP_TRY(hipMemsetAsync(cur.counts, 0, 2 * sizeof(int32_t), ln.stream));
+		HIP_TRY(hipEventRecord(ev[0], ln.stream));
+		HIP_TRY(rtamd::launch_closest(s->ds, ln.fg, L, n, remaining, cur, next, s->ctr, s->stats, ln.stream,
+		                              s->packet_mask));
+		cnt.stage_launches[0]++;
+		HIP_TRY(hipEventRecord(ev[1], ln.stream));
+		HIP_TRY(hipMemcpyAsync(ln.counts_host, cur.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ln.stream));
+		HIP_TRY(hipMemcpyAsync(ln.counts_host + 2, &s->ctr->error, sizeof(int32_t), hipMemcpyDeviceToHost, ln.stream));
+		HIP_TRY(hipEventRecord(ln.counts_ready, ln.stream));
+		ln.phase = Lane::TRACING;
+		return RT_OK;
+	}
+
+	// k_shadow + k_shade of the levels `lv` (their k_closest done) on stream q
+	int launch_shading(Lane& ln, const std::vector<std::pair<int, int64_t>>& lv, hipStream_t q) {
+		rtamd::ShadeBatch b{};
+		const int64_t nl = s->ds.n_nonambient;
+		auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
+		int64_t so = 0, ho = 0;
+		b.n = static_cast<int32_t>(lv.size());
+		for (int k = 0; k < b.n; k++) {
+			b.level[k] = lv[k].first;
+			b.nh[k] = lv[k].second;
+			b.shadow_begin[k] = so;
+			b.shade_begin[k] = ho;
+			so += wave_up(lv[k].second * nl);
+			ho += wave_up(lv[k].second);
+		}
+		b.shadow_begin[b.n] = so;
+		b.shade_begin[b.n] = ho;
+		const int first = lv.front().first, last = lv.back().first;
+		const auto& ev = ln.level_events[first];
+		HIP_TRY(hipStreamWaitEvent(q, ln.level_events[last][1], 0));
+		HIP_TRY(hipMemcpyAsync(ln.levels_dev, ln.levels_pinned, (last + 1) * sizeof(rtamd::RayLevel),
+		                       hipMemcpyHostToDevice, q));
+		HIP_TRY(hipEventRecord(ev[2], q));
+		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
+		if (nl > 0) cnt.stage_launches[1]++;
+		HIP_TRY(hipEventRecord(ev[3], q));
+		HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
+		cnt.stage_launches[2]++;
+		HIP_TRY(hipEventRecord(ev[4], q));
+		ln.shaded.push_back(first);
+		return RT_OK;
+	}
+
+	int start_chunk(Lane& ln, int64_t r0, int64_t rows, const rt_render_params* p) {
+		ln.fg = rtamd::FrameGeometry{};
+		ln.fg.width = p->width;
+		ln.fg.height = p->height;
+		ln.fg.row_begin = p->row_begin;
+		ln.fg.row_step = p->row_step;
+		ln.fg.chunk_row0 = static_cast<int32_t>(r0);
+		ln.fg.intersection_only = io;
+		ln.r0 = r0;
+		ln.n0 = rows * W;
+		ln.level = 0;
+		ln.level_n.assign(1, ln.n0);
+		ln.shaded.clear();
+		ln.deferred.clear();
+		int rc = ensure_level_record(s, ln, 0, ln.n0);
+		return rc ? rc : launch_level(ln);
+	}
+
+	// counts of the lane's level are on the host: shade it, launch the next level or
+	// finish the chunk.  Sets *error on a device MathException.
+	int on_counts(Lane& ln, bool* error) {
+		if (ln.counts_host[2]) {
+			*error = true;
+			ln.phase = Lane::IDLE;
+			return RT_OK;
+		}
+		const int L = ln.level;
+		cnt.trace_rays += ln.level_n[L];
+		const int64_t nh = ln.counts_host[0], nn = ln.counts_host[1];
+		int rc;
+		if (nh > 0) {
+			if (L < s->direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
+				if ((rc = launch_shading(ln, {{L, nh}}, ln.shade[L % 3]))) return rc;
+			} else {
+				ln.deferred.push_back({L, nh});
+			}
+		}
+		if (depth - L > 0 && nn > 0) {
+			ln.level_n.push_back(nn);
+			ln.level++;
+			return launch_level(ln);
+		}
+		for (size_t k = 0; k < ln.deferred.size(); k += rtamd::kMaxBatch) {
+			const size_t e = std::min(ln.deferred.size(), k + rtamd::kMaxBatch);
+			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, ln.shade[3]))) return rc;
+		}
+		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
+		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 0; l--)
+			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], ln.levels[l].lv, ln.levels[l + 1].lv, ln.stream));
+		HIP_TRY(rtamd::launch_output(ln.n0, ln.levels[0].lv, out_rgb_dev ? out_rgb_dev + ln.r0 * W * 3 : nullptr,
+		                             out_rgb8_dev ? out_rgb8_dev + ln.r0 * W * 3 : nullptr, io, s->stats, ln.stream));
+		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
+		ln.phase = Lane::FINISHING;
+		return RT_OK;
+	}
+
+	// the chunk's work is complete: per-kernel device times (events are re-recorded by
+	// the lane's next chunk)
+	int on_done(Lane& ln) {
+		for (int L = 0; L < static_cast<int>(ln.level_n.size()); L++) {
+			float ms = 0.f;
+			HIP_TRY(hipEventElapsedTime(&ms, ln.level_events[L][0], ln.level_events[L][1]));
+			cnt.stage_ms[0] += ms;
+			kernel_ms += ms;
+		}
+		for (int first : ln.shaded) {
+			const auto& ev = ln.level_events[first];
+			for (int k = 0; k < 2; k++) {
+				float ms = 0.f;
+				HIP_TRY(hipEventElapsedTime(&ms, ev[2 + k], ev[3 + k]));
+				cnt.stage_ms[1 + k] += ms;
+				kernel_ms += ms;
+			}
+		}
+		cnt.levels = std::max<int32_t>(cnt.levels, static_cast<int32_t>(ln.level_n.size()));
+		cnt.pixels += ln.n0;
+		ln.phase = Lane::IDLE;
+		return RT_OK;
+	}
+};
 
 int64_t selected_rows(const rt_render_params* p) {
 	if (p->row_step <= 0 || p->row_end <= p->row_begin) return 0;
@@ -229,14 +422,24 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
 	std::unique_ptr<rt_scene> s(new rt_scene());
 	s->device = device;
-	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);  // tuning knobs
+	int n_lanes = 1;  // measured: concurrent chunk pipelines are slower on C3
+	// tuning knobs
+	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);
 	if (const char* dl = std::getenv("RTAMD_DIRECT_LEVELS")) s->direct_levels = std::max(1, std::atoi(dl));
+	if (const char* nl = std::getenv("RTAMD_LANES")) n_lanes = std::min(8, std::max(1, std::atoi(nl)));
+	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
 	int prio_low = 0, prio_high = 0;
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_low, &prio_high));
-	HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, prio_high));
-	for (hipStream_t& q : s->shade_streams) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
+	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
-	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->counts_host), 4 * sizeof(int32_t), hipHostMallocDefault));
+	for (int k = 0; k < n_lanes; k++) {
+		s->lanes.emplace_back(new Lane());
+		int rc = lane_create(*s->lanes.back(), prio_low, prio_high);
+		if (rc) {
+			rt_scene_destroy(s.release());
+			return rc;
+		}
+	}
 	int rc;
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
@@ -283,18 +486,10 @@ void rt_scene_destroy(rt_scene* s) {
 	if (!s) return;
 	(void)hipSetDevice(s->device);
 	(void)hipDeviceSynchronize();
-	for (auto& L : s->levels)
-		if (L.block) (void)hipFree(L.block);
+	for (auto& ln : s->lanes) lane_destroy(*ln);
 	for (void* p : s->allocs) (void)hipFree(p);
 	if (s->out_dev) (void)hipFree(s->out_dev);
 	if (s->ctr_host) (void)hipHostFree(s->ctr_host);
-	if (s->counts_host) (void)hipHostFree(s->counts_host);
-	if (s->levels_pinned) (void)hipHostFree(s->levels_pinned);
-	if (s->levels_dev) (void)hipFree(s->levels_dev);
-	for (auto& ev : s->level_events)
-		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-	for (hipStream_t q : s->shade_streams)
-		if (q) (void)hipStreamDestroy(q);
 	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
 	delete s;
@@ -305,149 +500,56 @@ int rt_scene_get_info(const rt_scene* s, rt_scene_info* info) {
 	*info = s->info;
 	return RT_OK;
 }
-
 int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_dev, void* stream_v,
                      rt_counters* counters) {
 	int rc = check_params(s, p);
 	if (rc) return rc;
 	HIP_TRY(hipSetDevice(s->device));
-	// All work runs on the scene's streams; a caller's stream is joined first (its prior
-	// work, e.g. the allocation of the output buffers, completes before ours starts) and
-	// the call returns after the render stream has drained.
+	// The caller's stream is joined first (its prior work, e.g. the allocation of the
+	// output buffers, completes before ours starts); the call returns when all is done.
 	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
-	hipStream_t st = s->stream;
-	if (caller != st) {
-		HIP_TRY(hipEventRecord(s->fork_event, caller));
-		HIP_TRY(hipStreamWaitEvent(st, s->fork_event, 0));
-	}
 	const int64_t W = p->width;
 	const int64_t n_rows = selected_rows(p);
-	const int io = p->intersection_only != 0;
-	const int depth = io ? 0 : p->bounce_depth;
-	int64_t chunk_pixels = p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22;
-	const int64_t chunk_rows = std::max<int64_t>(1, chunk_pixels / W);
-	rt_counters cnt{};
-	cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
-	HIP_TRY(hipMemsetAsync(s->ctr, 0, sizeof(rtamd::DeviceCounters), st));
-	HIP_TRY(hipMemsetAsync(s->stats, 0, sizeof(unsigned long long) * s->stats_host.size(), st));
-	std::vector<int64_t> level_n;
-	float kernel_ms_total = 0.f;
-	for (int64_t r0 = 0; r0 < n_rows; r0 += chunk_rows) {
-		const int64_t rows = std::min(chunk_rows, n_rows - r0);
-		const int64_t n0 = rows * W;
-		rtamd::FrameGeometry fg{};
-		fg.width = p->width;
-		fg.height = p->height;
-		fg.row_begin = p->row_begin;
-		fg.row_step = p->row_step;
-		fg.chunk_row0 = static_cast<int32_t>(r0);
-		fg.intersection_only = io;
-		level_n.assign(1, n0);
-		if ((rc = ensure_level_record(s, 0, n0))) return rc;
-		std::vector<int> shaded;                            // first level of each shading launch
-		std::vector<std::pair<int, int64_t>> deferred;      // (level, hits) shaded after the chain
-		// k_shadow + k_shade of the levels `lv` (their k_closest done) on stream q
-		auto launch_shading = [&](const std::vector<std::pair<int, int64_t>>& lv, hipStream_t q) -> int {
-			rtamd::ShadeBatch b{};
-			const int64_t nl = s->ds.n_nonambient;
-			auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
-			int64_t so = 0, ho = 0;
-			b.n = static_cast<int32_t>(lv.size());
-			for (int k = 0; k < b.n; k++) {
-				b.level[k] = lv[k].first;
-				b.nh[k] = lv[k].second;
-				b.shadow_begin[k] = so;
-				b.shade_begin[k] = ho;
-				so += wave_up(lv[k].second * nl);
-				ho += wave_up(lv[k].second);
+	Render R{s, p->intersection_only ? 0 : p->bounce_depth, p->intersection_only != 0, out_rgb_dev, out_rgb8_dev, W};
+	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
+	HIP_TRY(hipMemsetAsync(s->ctr, 0, sizeof(rtamd::DeviceCounters), caller));
+	HIP_TRY(hipMemsetAsync(s->stats, 0, sizeof(unsigned long long) * s->stats_host.size(), caller));
+	HIP_TRY(hipEventRecord(s->fork_event, caller));
+	for (auto& ln : s->lanes) HIP_TRY(hipStreamWaitEvent(ln->stream, s->fork_event, 0));
+	// chunks: at most 4 M pixels (bounds the level buffers), and enough of them for every
+	// lane to hold `chunks_per_lane` of them
+	const int64_t max_rows = std::max<int64_t>(1, (p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22) / W);
+	const int64_t want = static_cast<int64_t>(s->lanes.size()) * (s->lanes.size() > 1 ? s->chunks_per_lane : 1);
+	const int64_t chunk_rows = std::min(max_rows, std::max<int64_t>(1, (n_rows + want - 1) / want));
+	int64_t next_row = 0;
+	bool error = false;
+	for (;;) {
+		bool busy = false;
+		for (auto& lp : s->lanes) {
+			Lane& ln = *lp;
+			if (ln.phase == Lane::IDLE) {
+				if (error || next_row >= n_rows) continue;
+				const int64_t rows = std::min(chunk_rows, n_rows - next_row);
+				if ((rc = R.start_chunk(ln, next_row, rows, p))) return rc;
+				next_row += rows;
+				busy = true;
+				continue;
 			}
-			b.shadow_begin[b.n] = so;
-			b.shade_begin[b.n] = ho;
-			const int first = lv.front().first, last = lv.back().first;
-			const auto& ev = s->level_events[first];
-			HIP_TRY(hipStreamWaitEvent(q, s->level_events[last][1], 0));
-			HIP_TRY(hipMemcpyAsync(s->levels_dev, s->levels_pinned, (last + 1) * sizeof(rtamd::RayLevel),
-			                       hipMemcpyHostToDevice, q));
-			HIP_TRY(hipEventRecord(ev[2], q));
-			HIP_TRY(rtamd::launch_shadow(s->ds, b, s->levels_dev, s->ctr, s->stats, q, s->packet_mask));
-			if (nl > 0) cnt.stage_launches[1]++;
-			HIP_TRY(hipEventRecord(ev[3], q));
-			HIP_TRY(rtamd::launch_shade(s->ds, fg, b, s->levels_dev, s->ctr, q));
-			cnt.stage_launches[2]++;
-			HIP_TRY(hipEventRecord(ev[4], q));
-			shaded.push_back(first);
-			return RT_OK;
-		};
-		bool error = false;
-		for (int L = 0;; L++) {
-			const int remaining = depth - L;
-			const int64_t n = level_n[L];
-			if (remaining > 0 && (rc = ensure_level_record(s, L + 1, 2 * n))) return rc;
-			if ((rc = ensure_events(s, L))) return rc;
-			const auto& ev = s->level_events[L];
-			const rtamd::RayLevel& cur = s->levels[L].lv;
-			const rtamd::RayLevel& next = remaining > 0 ? s->levels[L + 1].lv : cur;
-			HIP_TRY(hipMemsetAsync(cur.counts, 0, 2 * sizeof(int32_t), st));
-			HIP_TRY(hipEventRecord(ev[0], st));
-			HIP_TRY(rtamd::launch_closest(s->ds, fg, L, n, remaining, cur, next, s->ctr, s->stats, st, s->packet_mask));
-			cnt.stage_launches[0]++;
-			HIP_TRY(hipEventRecord(ev[1], st));
-			HIP_TRY(hipMemcpyAsync(s->counts_host, cur.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
-			HIP_TRY(hipMemcpyAsync(s->counts_host + 2, &s->ctr->error, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-			HIP_TRY(hipStreamSynchronize(st));
-			if (s->counts_host[2]) {
-				error = true;
-				break;
-			}
-			cnt.trace_rays += n;
-			const int64_t nh = s->counts_host[0], nn = s->counts_host[1];
-			if (nh > 0) {
-				if (L < s->direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
-					if ((rc = launch_shading({{L, nh}}, s->shade_streams[L % 3]))) return rc;
-				} else {
-					deferred.push_back({L, nh});
-				}
-			}
-			if (remaining <= 0 || nn == 0) break;
-			level_n.push_back(nn);
+			busy = true;
+			hipEvent_t e = ln.phase == Lane::TRACING ? ln.counts_ready : ln.chunk_done;
+			const hipError_t q = hipEventQuery(e);
+			if (q == hipErrorNotReady) continue;
+			if (q != hipSuccess) return fail(RT_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));
+			rc = ln.phase == Lane::TRACING ? R.on_counts(ln, &error) : R.on_done(ln);
+			if (rc) return rc;
 		}
-		if (error) {
-			HIP_TRY(hipDeviceSynchronize());
-			break;
-		}
-		for (size_t k = 0; k < deferred.size(); k += rtamd::kMaxBatch) {
-			const size_t e = std::min(deferred.size(), k + rtamd::kMaxBatch);
-			if ((rc = launch_shading({deferred.begin() + k, deferred.begin() + e}, s->shade_streams[3]))) return rc;
-		}
-		for (int L : shaded) HIP_TRY(hipStreamWaitEvent(st, s->level_events[L][4], 0));
-		for (int L = static_cast<int>(level_n.size()) - 2; L >= 0; L--)
-			HIP_TRY(rtamd::launch_reduce_level(level_n[L], s->levels[L].lv, s->levels[L + 1].lv, st));
-		HIP_TRY(rtamd::launch_output(n0, s->levels[0].lv, out_rgb_dev ? out_rgb_dev + r0 * W * 3 : nullptr,
-		                             out_rgb8_dev ? out_rgb8_dev + r0 * W * 3 : nullptr, io, s->stats, st));
-		// per-kernel device times of this chunk (events are re-recorded by the next chunk)
-		HIP_TRY(hipStreamSynchronize(st));
-		for (int L = 0; L < static_cast<int>(level_n.size()); L++) {
-			const auto& ev = s->level_events[L];
-			float ms = 0.f;
-			HIP_TRY(hipEventElapsedTime(&ms, ev[0], ev[1]));
-			cnt.stage_ms[0] += ms;
-			kernel_ms_total += ms;
-		}
-		for (int L : shaded) {
-			const auto& ev = s->level_events[L];
-			for (int k = 0; k < 2; k++) {
-				float ms = 0.f;
-				HIP_TRY(hipEventElapsedTime(&ms, ev[2 + k], ev[3 + k]));
-				cnt.stage_ms[1 + k] += ms;
-				kernel_ms_total += ms;
-			}
-		}
-		cnt.levels = std::max<int32_t>(cnt.levels, static_cast<int32_t>(level_n.size()));
-		cnt.pixels += n0;
+		if (!busy) break;
 	}
-	HIP_TRY(hipMemcpyAsync(s->ctr_host, s->ctr, sizeof(rtamd::DeviceCounters), hipMemcpyDeviceToHost, st));
-	HIP_TRY(hipStreamSynchronize(st));
+	HIP_TRY(hipDeviceSynchronize());  // includes the shading of a chunk stopped by an error
+	HIP_TRY(hipMemcpy(s->ctr_host, s->ctr, sizeof(rtamd::DeviceCounters), hipMemcpyDeviceToHost));
 	if (s->ctr_host->error) return fail(RT_ERR_MATH, device_error_text(s->ctr_host->error));
+	rt_counters& cnt = R.cnt;
+	const int io = R.io;
 	HIP_TRY(hipMemcpy(s->stats_host.data(), s->stats, sizeof(unsigned long long) * s->stats_host.size(),
 	                  hipMemcpyDeviceToHost));
 	unsigned long long sum[rtamd::ST_COUNT] = {0};
@@ -478,11 +580,11 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		std::memcpy(&m, &b, sizeof(m));
 		cnt.intersection_max = std::max(cnt.intersection_max, m);
 	}
-	cnt.kernel_ms = kernel_ms_total;
+	cnt.kernel_ms = R.kernel_ms;
 	// full-image --intersection-only: normalise in place (scene.cpp:50-58)
 	if (io && p->row_begin == 0 && p->row_end == p->height && p->row_step == 1 && out_rgb_dev) {
-		HIP_TRY(rtamd::launch_normalize(n_rows * W * 3, out_rgb_dev, cnt.intersection_max, out_rgb8_dev, st));
-		HIP_TRY(hipStreamSynchronize(st));
+		HIP_TRY(rtamd::launch_normalize(n_rows * W * 3, out_rgb_dev, cnt.intersection_max, out_rgb8_dev, caller));
+		HIP_TRY(hipStreamSynchronize(caller));
 	}
 	if (counters) *counters = cnt;
 	return RT_OK;
