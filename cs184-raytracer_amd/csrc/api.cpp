@@ -73,7 +73,7 @@ struct Lane {
 	std::vector<std::array<hipEvent_t, 5>> level_events;
 	hipEvent_t counts_ready = nullptr;   // level counts copied to counts_host
 	hipEvent_t chunk_done = nullptr;     // output of the chunk written
-	int32_t* counts_host = nullptr;      // pinned: hits, children, error word
+	int32_t* counts_host = nullptr;      // pinned: hits, children
 	// chunk state
 	enum Phase { IDLE, TRACING, FINISHING } phase = IDLE;
 	rtamd::FrameGeometry fg{};
@@ -166,18 +166,26 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
 		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), hipHostMallocDefault));
 		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dev), cap * sizeof(rtamd::RayLevel)));
+		std::memset(pin, 0, cap * sizeof(rtamd::RayLevel));
 		if (ln.levels_pinned) {
 			std::memcpy(pin, ln.levels_pinned, ln.levels_cap * sizeof(rtamd::RayLevel));
 			(void)hipHostFree(ln.levels_pinned);
 			(void)hipFree(ln.levels_dev);
 		}
+		HIP_TRY(hipMemcpy(dev, pin, cap * sizeof(rtamd::RayLevel), hipMemcpyHostToDevice));
 		ln.levels_pinned = pin;
 		ln.levels_dev = dev;
 		ln.levels_cap = cap;
 	}
 	int rc = ensure_level(s, ln, level, capacity);
 	if (rc) return rc;
-	ln.levels_pinned[level] = ln.levels[level].lv;
+	if (std::memcmp(&ln.levels_pinned[level], &ln.levels[level].lv, sizeof(rtamd::RayLevel)) != 0) {
+		// new buffers: the device copy is updated in stream order, ahead of any kernel of
+		// this level (the entry itself changes only after a device-wide synchronisation)
+		ln.levels_pinned[level] = ln.levels[level].lv;
+		HIP_TRY(hipMemcpyAsync(ln.levels_dev + level, ln.levels_pinned + level, sizeof(rtamd::RayLevel),
+		                       hipMemcpyHostToDevice, ln.stream));
+	}
 	return RT_OK;
 }
 
@@ -236,14 +244,14 @@ struct Render {
 		const auto& ev = ln.level_events[L];
 		const rtamd::RayLevel& cur = ln.levels[L].lv;
 		const rtamd::RayLevel& next = remaining > 0 ? ln.levels[L + 1].lv : cur;
-		HIP_TRY(hipMemsetAsync(cur.counts, 0, 2 * sizeof(int32_t), ln.stream));
+		// level 0's counts are cleared here, deeper ones by the previous level's k_closest
+		if (L == 0) HIP_TRY(hipMemsetAsync(cur.counts, 0, 2 * sizeof(int32_t), ln.stream));
 		HIP_TRY(hipEventRecord(ev[0], ln.stream));
 		HIP_TRY(rtamd::launch_closest(s->ds, ln.fg, L, n, remaining, cur, next, s->ctr, s->stats, ln.stream,
 		                              s->packet_mask));
 		cnt.stage_launches[0]++;
 		HIP_TRY(hipEventRecord(ev[1], ln.stream));
 		HIP_TRY(hipMemcpyAsync(ln.counts_host, cur.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ln.stream));
-		HIP_TRY(hipMemcpyAsync(ln.counts_host + 2, &s->ctr->error, sizeof(int32_t), hipMemcpyDeviceToHost, ln.stream));
 		HIP_TRY(hipEventRecord(ln.counts_ready, ln.stream));
 		ln.phase = Lane::TRACING;
 		return RT_OK;
@@ -269,8 +277,6 @@ struct Render {
 		const int first = lv.front().first, last = lv.back().first;
 		const auto& ev = ln.level_events[first];
 		HIP_TRY(hipStreamWaitEvent(q, ln.level_events[last][1], 0));
-		HIP_TRY(hipMemcpyAsync(ln.levels_dev, ln.levels_pinned, (last + 1) * sizeof(rtamd::RayLevel),
-		                       hipMemcpyHostToDevice, q));
 		HIP_TRY(hipEventRecord(ev[2], q));
 		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) cnt.stage_launches[1]++;
@@ -300,18 +306,21 @@ struct Render {
 		return rc ? rc : launch_level(ln);
 	}
 
-	// counts of the lane's level are on the host: shade it, launch the next level or
-	// finish the chunk.  Sets *error on a device MathException.
-	int on_counts(Lane& ln, bool* error) {
-		if (ln.counts_host[2]) {
-			*error = true;
-			ln.phase = Lane::IDLE;
-			return RT_OK;
-		}
+	// counts of the lane's level are on the host: launch the next level (the critical
+	// path) first, then the shading of this one, or finish the chunk.  A device
+	// MathException is reported after the render (the reference aborts; the GPU merely
+	// finishes the chunk).
+	int on_counts(Lane& ln) {
 		const int L = ln.level;
 		cnt.trace_rays += ln.level_n[L];
 		const int64_t nh = ln.counts_host[0], nn = ln.counts_host[1];
 		int rc;
+		const bool more = depth - L > 0 && nn > 0;
+		if (more) {
+			ln.level_n.push_back(nn);
+			ln.level++;
+			if ((rc = launch_level(ln))) return rc;
+		}
 		if (nh > 0) {
 			if (L < s->direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
 				if ((rc = launch_shading(ln, {{L, nh}}, ln.shade[L % 3]))) return rc;
@@ -319,11 +328,7 @@ struct Render {
 				ln.deferred.push_back({L, nh});
 			}
 		}
-		if (depth - L > 0 && nn > 0) {
-			ln.level_n.push_back(nn);
-			ln.level++;
-			return launch_level(ln);
-		}
+		if (more) return RT_OK;
 		for (size_t k = 0; k < ln.deferred.size(); k += rtamd::kMaxBatch) {
 			const size_t e = std::min(ln.deferred.size(), k + rtamd::kMaxBatch);
 			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, ln.shade[3]))) return rc;
@@ -522,13 +527,12 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 	const int64_t want = static_cast<int64_t>(s->lanes.size()) * (s->lanes.size() > 1 ? s->chunks_per_lane : 1);
 	const int64_t chunk_rows = std::min(max_rows, std::max<int64_t>(1, (n_rows + want - 1) / want));
 	int64_t next_row = 0;
-	bool error = false;
 	for (;;) {
 		bool busy = false;
 		for (auto& lp : s->lanes) {
 			Lane& ln = *lp;
 			if (ln.phase == Lane::IDLE) {
-				if (error || next_row >= n_rows) continue;
+				if (next_row >= n_rows) continue;
 				const int64_t rows = std::min(chunk_rows, n_rows - next_row);
 				if ((rc = R.start_chunk(ln, next_row, rows, p))) return rc;
 				next_row += rows;
@@ -540,12 +544,12 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 			const hipError_t q = hipEventQuery(e);
 			if (q == hipErrorNotReady) continue;
 			if (q != hipSuccess) return fail(RT_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));
-			rc = ln.phase == Lane::TRACING ? R.on_counts(ln, &error) : R.on_done(ln);
+			rc = ln.phase == Lane::TRACING ? R.on_counts(ln) : R.on_done(ln);
 			if (rc) return rc;
 		}
 		if (!busy) break;
 	}
-	HIP_TRY(hipDeviceSynchronize());  // includes the shading of a chunk stopped by an error
+	HIP_TRY(hipDeviceSynchronize());
 	HIP_TRY(hipMemcpy(s->ctr_host, s->ctr, sizeof(rtamd::DeviceCounters), hipMemcpyDeviceToHost));
 	if (s->ctr_host->error) return fail(RT_ERR_MATH, device_error_text(s->ctr_host->error));
 	rt_counters& cnt = R.cnt;

@@ -165,6 +165,8 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScen
 	const int64_t t = xcd_block() * kBlock + threadIdx.x;
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
+	// the next level's counts start at zero (its k_closest appends to them)
+	if (remaining > 0 && blockIdx.x == 0 && threadIdx.x == 0) next.counts[0] = next.counts[1] = 0;
 	WorkStats ws{0, 0, 0, 0, 0};
 	bool hit = false;
 	int gi = -1;
