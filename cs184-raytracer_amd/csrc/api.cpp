@@ -67,19 +67,19 @@ struct Lane {
 	rtamd::RayLevel* levels_pinned = nullptr;
 	rtamd::RayLevel* levels_dev = nullptr;
 	size_t levels_cap = 0;
-	// per level: [0] before k_closest, [1] after it (the shading streams wait on it);
-	// per shading launch, in the events of its first level: [2] before k_shadow, [3] after
-	// it, [4] after k_shade (the reduce waits on it)
-	std::vector<std::array<hipEvent_t, 5>> level_events;
-	hipEvent_t counts_ready = nullptr;   // level counts copied to counts_host
+	// per level: [0] before k_closest, [1] after it (the shading streams wait on it),
+	// [5] the level's counts copied to counts_host; per shading launch, in the events of
+	// its first level: [2] before k_shadow, [3] after it, [4] after k_shade (the reduce
+	// waits on it)
+	std::vector<std::array<hipEvent_t, 6>> level_events;
 	hipEvent_t chunk_done = nullptr;     // output of the chunk written
-	int32_t* counts_host = nullptr;      // pinned: hits, children
+	int32_t* counts_host = nullptr;      // pinned, per level: hits, children (levels_cap x 2)
 	// chunk state
 	enum Phase { IDLE, TRACING, FINISHING } phase = IDLE;
 	rtamd::FrameGeometry fg{};
 	int64_t r0 = 0, n0 = 0;
-	int level = 0;
-	std::vector<int64_t> level_n;
+	int level = 0;                        // the level whose counts are awaited
+	std::vector<int64_t> level_n;         // ray counts of the levels known so far
 	std::vector<int> shaded;                        // first level of each shading launch
 	std::vector<std::pair<int, int64_t>> deferred;  // (level, hits) shaded after the chain
 };
@@ -164,14 +164,19 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		HIP_TRY(hipDeviceSynchronize());
 		const size_t cap = std::max<size_t>(16, 2 * (level + 1));
 		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
+		int32_t* counts = nullptr;
 		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), hipHostMallocDefault));
 		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dev), cap * sizeof(rtamd::RayLevel)));
+		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&counts), 2 * cap * sizeof(int32_t), hipHostMallocDefault));
 		std::memset(pin, 0, cap * sizeof(rtamd::RayLevel));
 		if (ln.levels_pinned) {
 			std::memcpy(pin, ln.levels_pinned, ln.levels_cap * sizeof(rtamd::RayLevel));
+			std::memcpy(counts, ln.counts_host, 2 * ln.levels_cap * sizeof(int32_t));
 			(void)hipHostFree(ln.levels_pinned);
+			(void)hipHostFree(ln.counts_host);
 			(void)hipFree(ln.levels_dev);
 		}
+		ln.counts_host = counts;
 		HIP_TRY(hipMemcpy(dev, pin, cap * sizeof(rtamd::RayLevel), hipMemcpyHostToDevice));
 		ln.levels_pinned = pin;
 		ln.levels_dev = dev;
@@ -191,7 +196,7 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 
 int ensure_events(Lane& ln, size_t level) {
 	while (ln.level_events.size() <= level) {
-		std::array<hipEvent_t, 5> ev{};
+		std::array<hipEvent_t, 6> ev{};
 		for (hipEvent_t& e : ev) HIP_TRY(hipEventCreate(&e));
 		ln.level_events.push_back(ev);
 	}
@@ -201,9 +206,7 @@ int ensure_events(Lane& ln, size_t level) {
 int lane_create(Lane& ln, int prio_low, int prio_high) {
 	HIP_TRY(hipStreamCreateWithPriority(&ln.stream, hipStreamNonBlocking, prio_high));
 	for (hipStream_t& q : ln.shade) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
-	HIP_TRY(hipEventCreateWithFlags(&ln.counts_ready, hipEventDisableTiming));
 	HIP_TRY(hipEventCreateWithFlags(&ln.chunk_done, hipEventDisableTiming));
-	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.counts_host), 4 * sizeof(int32_t), hipHostMallocDefault));
 	return RT_OK;
 }
 
@@ -215,7 +218,6 @@ void lane_destroy(Lane& ln) {
 	if (ln.counts_host) (void)hipHostFree(ln.counts_host);
 	for (auto& ev : ln.level_events)
 		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-	if (ln.counts_ready) (void)hipEventDestroy(ln.counts_ready);
 	if (ln.chunk_done) (void)hipEventDestroy(ln.chunk_done);
 	for (hipStream_t q : ln.shade)
 		if (q) (void)hipStreamDestroy(q);
@@ -233,12 +235,13 @@ struct Render {
 	rt_counters cnt{};
 	float kernel_ms = 0.f;
 
-	// k_closest of the lane's current level, then the counts read-back
-	int launch_level(Lane& ln) {
-		const int L = ln.level;
+	// k_closest of level L, then the read-back of its counts.  n: the level's ray count, or
+	// with n_dev (the previous level's child counter) an upper bound: the level is queued
+	// behind the previous one before the host knows its size (one level of lookahead).
+	int launch_closest_level(Lane& ln, int L, int64_t n, const int32_t* n_dev) {
 		const int remaining = depth - L;
-		const int64_t n = ln.level_n[L];
 		int rc;
+		// children of this level: at most 2 per ray
 		if (remaining > 0 && (rc = ensure_level_record(s, ln, L + 1, 2 * n))) return rc;
 		if ((rc = ensure_events(ln, L))) return rc;
 		const auto& ev = ln.level_events[L];
@@ -247,13 +250,13 @@ struct Render {
 		// level 0's counts are cleared here, deeper ones by the previous level's k_closest
 		if (L == 0) HIP_TRY(hipMemsetAsync(cur.counts, 0, 2 * sizeof(int32_t), ln.stream));
 		HIP_TRY(hipEventRecord(ev[0], ln.stream));
-		HIP_TRY(rtamd::launch_closest(s->ds, ln.fg, L, n, remaining, cur, next, s->ctr, s->stats, ln.stream,
+		HIP_TRY(rtamd::launch_closest(s->ds, ln.fg, L, n, n_dev, remaining, cur, next, s->ctr, s->stats, ln.stream,
 		                              s->packet_mask));
 		cnt.stage_launches[0]++;
 		HIP_TRY(hipEventRecord(ev[1], ln.stream));
-		HIP_TRY(hipMemcpyAsync(ln.counts_host, cur.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ln.stream));
-		HIP_TRY(hipEventRecord(ln.counts_ready, ln.stream));
-		ln.phase = Lane::TRACING;
+		HIP_TRY(hipMemcpyAsync(ln.counts_host + 2 * L, cur.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
+		                       ln.stream));
+		HIP_TRY(hipEventRecord(ev[5], ln.stream));
 		return RT_OK;
 	}
 
@@ -302,8 +305,11 @@ struct Render {
 		ln.level_n.assign(1, ln.n0);
 		ln.shaded.clear();
 		ln.deferred.clear();
+		ln.phase = Lane::TRACING;
 		int rc = ensure_level_record(s, ln, 0, ln.n0);
-		return rc ? rc : launch_level(ln);
+		if (!rc) rc = launch_closest_level(ln, 0, ln.n0, nullptr);
+		if (!rc && depth >= 1) rc = launch_closest_level(ln, 1, 2 * ln.n0, ln.levels[0].lv.counts + 1);
+		return rc;
 	}
 
 	// counts of the lane's level are on the host: launch the next level (the critical
@@ -313,13 +319,16 @@ struct Render {
 	int on_counts(Lane& ln) {
 		const int L = ln.level;
 		cnt.trace_rays += ln.level_n[L];
-		const int64_t nh = ln.counts_host[0], nn = ln.counts_host[1];
+		const int64_t nh = ln.counts_host[2 * L], nn = ln.counts_host[2 * L + 1];
 		int rc;
+		// k_closest(L+1) is already queued; queue k_closest(L+2) behind it
 		const bool more = depth - L > 0 && nn > 0;
 		if (more) {
 			ln.level_n.push_back(nn);
 			ln.level++;
-			if ((rc = launch_level(ln))) return rc;
+			if (L + 2 <= depth &&
+			    (rc = launch_closest_level(ln, L + 2, 2 * nn, ln.levels[L + 1].lv.counts + 1)))
+				return rc;
 		}
 		if (nh > 0) {
 			if (L < s->direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
@@ -540,7 +549,7 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 				continue;
 			}
 			busy = true;
-			hipEvent_t e = ln.phase == Lane::TRACING ? ln.counts_ready : ln.chunk_done;
+			hipEvent_t e = ln.phase == Lane::TRACING ? ln.level_events[ln.level][5] : ln.chunk_done;
 			const hipError_t q = hipEventQuery(e);
 			if (q == hipErrorNotReady) continue;
 			if (q != hipSuccess) return fail(RT_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));

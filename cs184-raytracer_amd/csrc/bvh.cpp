@@ -365,12 +365,9 @@ FlatScene flatten_scene(const Scene& s) {
 		// Conservative padding: the traversal may prune a node only when no face inside it
 		// can pass the reference's Cramer test; 1e-9 of the largest coordinate magnitude is
 		// ~10^7 ulps of slack for the fp64 slab and Cramer rounding (validated bit-exact
-		// against the oracle over every shipped scene).  The fp32 slab test adds 2^-15 of
-		// it: rounding the ray origin o to fp32 and the fma form fma(lo, I, -fl(O*I)) move
-		// a slab plane by at most 2^-23 |o_axis| (1 + 2^-20), which this padding absorbs
-		// for |o_axis| <= 128 amax (= o_limit; intersect.h, slab32).
-		const double pad = 1e-9 * amax + 0x1p-15 * amax + 1e-300;
-		d.o_limit = 128.0 * amax;
+		// against the oracle over every shipped scene).  The padded boxes are then
+		// rounded outward to fp32 (DBvhNode).
+		const double pad = 1e-9 * amax + 1e-300;
 		const size_t node_base = fs.nodes.size();
 		for (int attempt = 0; attempt < 2; attempt++) {
 			fs.nodes.resize(node_base);

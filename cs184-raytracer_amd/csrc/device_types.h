@@ -41,11 +41,6 @@ struct alignas(16) DGeom {
 	// "ray has no direction" (rtbase.h:17-23): every ray must then check this geometry,
 	// even where culling or an early exit would skip it (bvh.cpp, intersect.h).
 	int32_t may_raise;
-	// The fp32 node slab test is conservative for object-space ray origins with every
-	// |coordinate| <= o_limit (the node boxes carry the padding for that); rays from
-	// farther away use the fp64 slab test on the same boxes (intersect.h).
-	double o_limit;
-	double pad2;
 };
 
 struct alignas(16) DMaterial {   // rtbase.h:30-39

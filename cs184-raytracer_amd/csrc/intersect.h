@@ -22,14 +22,6 @@ namespace dev {
 
 constexpr int kBlock = 128;  // 2 waves; LDS traversal stack = kStackDepth x kBlock x (4 + 4) B
 
-#ifndef RT_WHILE_WHILE
-#define RT_WHILE_WHILE 1
-#endif
-// per-lane traversal stack words per entry: node ref (+ entry distance with RT_POP_PRUNE)
-#ifndef RT_POP_PRUNE
-#define RT_POP_PRUNE 0
-#endif
-constexpr int kStackWords = (RT_WHILE_WHILE && RT_POP_PRUNE) ? 2 : 1;
 
 // Scene data read at a wave-uniform address goes through the constant address space so
 // it is fetched with scalar (SMEM) loads into SGPRs: one fetch per wave, no VGPRs.
@@ -213,70 +205,7 @@ __device__ __forceinline__ V3 safe_inv(V3 d) {
 
 __device__ __forceinline__ double prune_limit(double best_dist) { return best_dist * (1.0 + 4e-9); }
 
-// ---------------------------------------------------------------- fp32 node slab test
-// Conservative fp32 form of slab() for the fp32 node boxes (bvh.cpp): with O = fl32(o),
-// I = fl32(fl64(1/d)) and t = fma(lo, I, -fl32(O * I)), each computed plane distance is
-// the exact distance to a plane moved by at most 2^-23 |o_axis| (absorbed by the box
-// padding while |o_axis| <= o_limit), times a factor within 1 +- 2^-22 (absorbed by the
-// relative widening 2^-20).  |I| is clamped to 2^60: for a direction component below
-// 2^-60 the clamped distances to the padded planes still exceed any face distance.
-// No NaN can arise except from widening an infinite entry/exit, which is a true miss.
-struct Ray32 {
-	float ix, iy, iz;     // I
-	float oix, oiy, oiz;  // fl32(O * I)
-};
-__device__ __forceinline__ float clamp_inv(double inv) {
-	return fminf(fmaxf(static_cast<float>(inv), -0x1p60f), 0x1p60f);
-}
-__device__ __forceinline__ Ray32 ray32(V3 o, V3 inv) {
-	Ray32 r;
-	r.ix = clamp_inv(inv.x);
-	r.iy = clamp_inv(inv.y);
-	r.iz = clamp_inv(inv.z);
-	r.oix = static_cast<float>(o.x) * r.ix;
-	r.oiy = static_cast<float>(o.y) * r.iy;
-	r.oiz = static_cast<float>(o.z) * r.iz;
-	return r;
-}
-// the fp32 slab test is valid for this object-space origin (bvh.cpp, o_limit)
-#ifndef RT_NODE_F32
-#define RT_NODE_F32 0
-#endif
-__device__ __forceinline__ bool origin_fits_f32(V3 o, double o_limit) {
-	if (!RT_NODE_F32) return false;
-	return fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) <= o_limit;
-}
-// lim rounded up to fp32
-__device__ __forceinline__ float limit_f32(double lim) {
-	float f = static_cast<float>(lim);
-	if (static_cast<double>(f) < lim)  // next float up (f is finite here)
-		f = f == 0.0f ? 0x1p-149f : __uint_as_float(__float_as_uint(f) + (f > 0.0f ? 1u : 0xffffffffu));
-	return f;
-}
-template <typename P>
-__device__ __forceinline__ bool slab32(P lo, P hi, const Ray32& r, float lim, float& tnear) {
-	const float tx0 = fmaf(lo[0], r.ix, -r.oix), tx1 = fmaf(hi[0], r.ix, -r.oix);
-	const float ty0 = fmaf(lo[1], r.iy, -r.oiy), ty1 = fmaf(hi[1], r.iy, -r.oiy);
-	const float tz0 = fmaf(lo[2], r.iz, -r.oiz), tz1 = fmaf(hi[2], r.iz, -r.oiz);
-	float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-	float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-	tmin = fmaf(-fabsf(tmin), 0x1p-20f, tmin);
-	tmax = fmaf(fabsf(tmax), 0x1p-20f, tmax);
-	tnear = tmin;
-	return tmax >= tmin && tmax >= 0.0f && tmin <= lim;
-}
-// one child box of a node: fp32 test, or fp64 on the same boxes for far origins
-template <typename P>
-__device__ __forceinline__ bool node_slab(P lo, P hi, bool f32, const Ray32& r, float lim32, V3 o, V3 inv, double lim,
-                                          double& tnear) {
-	if (f32) {
-		float t;
-		const bool h = slab32(lo, hi, r, lim32, t);
-		tnear = t;
-		return h;
-	}
-	return slab(lo, hi, o, inv, lim, tnear);
-}
+
 
 // Mesh::calculateIntNormInObjSpace (geometry.cpp:69-126) with an LBVH in place of the
 // linear scan for large meshes.
@@ -304,42 +233,24 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 				return true;
 			}
 	} else {
-#if RT_WHILE_WHILE
 		// while-while traversal (Aila & Laine 2009): a lane first walks inner nodes until
 		// it holds a leaf, then the lanes holding leaves test their faces together, so
 		// node and face work do not interleave within a wave.  `ref` >= 0 is a node,
-		// <= -2 a leaf (face offset << 3 | count), -1 done.  The stack keeps each far
-		// child's entry distance (rounded down to float) so that a popped subtree the
-		// search has since pruned (it begins beyond the best face) is skipped.
+		// <= -2 a leaf (face offset << 3 | count), -1 done.  The far child of a node whose
+		// two children are hit is pushed (LDS stack, kStackDepth entries per lane).
 		ws.bvh_entries++;
 		const V3 inv = safe_inv(d);
-		const Ray32 r32 = ray32(o, inv);
-		const bool f32 = origin_fits_f32(o, G->o_limit);
-		float* tstack = reinterpret_cast<float*>(stack + kStackDepth * kBlock);
-		(void)tstack;
 		int32_t ref = G->bvh_root;
 		int sp = 0;
-		auto pop = [&]() {
-#if RT_POP_PRUNE
-			const double lim = fmin(prune_limit(best.dist), prune_cap);
-			while (sp > 0) {
-				--sp;
-				if ((double)tstack[sp * kBlock] <= lim) return stack[sp * kBlock];
-			}
-			return (int32_t)-1;
-#else
-			return sp > 0 ? stack[--sp * kBlock] : (int32_t)-1;
-#endif
-		};
+		auto pop = [&]() { return sp > 0 ? stack[--sp * kBlock] : (int32_t)-1; };
 		while (ref != -1) {
 			while (ref >= 0) {
 				ws.nodes++;
 				const DBvhNode* N = S.nodes + ref;
 				double tn0, tn1;
 				const double lim = fmin(prune_limit(best.dist), prune_cap);
-				const float lim32 = limit_f32(lim);
-				const bool h0 = node_slab(N->lo[0], N->hi[0], f32, r32, lim32, o, inv, lim, tn0);
-				const bool h1 = node_slab(N->lo[1], N->hi[1], f32, r32, lim32, o, inv, lim, tn1);
+				const bool h0 = slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
+				const bool h1 = slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
 				if (h0 || h1) {
 					const int c = (h0 && h1) ? (tn1 < tn0 ? 1 : 0) : (h1 ? 1 : 0);
 					const int32_t cf = N->first[c], cc = N->count[c];
@@ -348,9 +259,6 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 						const int32_t ff = N->first[c ^ 1], fc = N->count[c ^ 1];
 						if (sp < kStackDepth) {
 							stack[sp * kBlock] = fc > 0 ? -2 - ((ff << 3) | fc) : ff;
-#if RT_POP_PRUNE
-							tstack[sp * kBlock] = __double2float_rd(c ? tn0 : tn1);
-#endif
 							sp++;
 						} else {
 							raise_error(ctr, DERR_STACK);
@@ -372,51 +280,6 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 			ref = pop();
 		}
 	}
-#else
-		const V3 inv = safe_inv(d);
-		const Ray32 r32 = ray32(o, inv);
-		const bool f32 = origin_fits_f32(o, G->o_limit);
-		int32_t node = G->bvh_root;
-		int sp = 0;
-		for (;;) {
-			ws.nodes++;
-			const DBvhNode* N = S.nodes + node;
-			double tn0, tn1;
-			const double lim = fmin(prune_limit(best.dist), prune_cap);
-			const float lim32 = limit_f32(lim);
-			const bool h0 = node_slab(N->lo[0], N->hi[0], f32, r32, lim32, o, inv, lim, tn0);
-			const bool h1 = node_slab(N->lo[1], N->hi[1], f32, r32, lim32, o, inv, lim, tn1);
-			const int first = (h0 && h1 && tn1 < tn0) ? 1 : 0;
-			int32_t next = -1;
-#pragma unroll
-			for (int k = 0; k < 2; k++) {
-				const int c = first ^ k;
-				if (!(c ? h1 : h0)) continue;
-				if (k == 1 && (c ? tn1 : tn0) > fmin(prune_limit(best.dist), prune_cap)) continue;
-				const int32_t cf = N->first[c], cc = N->count[c];
-				if (cc > 0) {
-					const int32_t f0 = G->face_begin + cf;
-					for (int32_t f = f0; f < f0 + cc; f++)
-						if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
-							settled = true;
-							return true;
-						}
-				} else if (next < 0) {
-					next = cf;
-				} else if (sp < kStackDepth) {
-					stack[sp++ * kBlock] = cf;
-				} else {
-					raise_error(ctr, DERR_STACK);
-				}
-			}
-			if (next < 0) {
-				if (sp == 0) break;
-				next = stack[--sp * kBlock];
-			}
-			node = next;
-		}
-	}
-#endif
 	found_dist = best.dist;
 	if (best.face < 0) return false;
 	const DFaceGeo* F = S.fgeo + best.face;
@@ -581,8 +444,6 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 		} else {
 			if (live) ws.bvh_entries++;
 			const V3 inv = safe_inv(d);
-			const Ray32 r32 = ray32(o, inv);
-			const bool f32 = origin_fits_f32(o, G->o_limit);
 			const auto nodes = uniform_ptr(S.nodes);
 			int32_t node = G->bvh_root;
 			int sp = 0;
@@ -591,9 +452,8 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				if (live) ws.nodes++;
 				double tn0 = 0, tn1 = 0;
 				const double lim = fmin(prune_limit(best.dist), prune_cap);
-				const float lim32 = limit_f32(lim);
-				const bool h0 = live && node_slab(N->lo[0], N->hi[0], f32, r32, lim32, o, inv, lim, tn0);
-				const bool h1 = live && node_slab(N->lo[1], N->hi[1], f32, r32, lim32, o, inv, lim, tn1);
+				const bool h0 = live && slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
+				const bool h1 = live && slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
 				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
 				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
 				const int first = (2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0;

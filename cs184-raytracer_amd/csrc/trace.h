@@ -77,9 +77,11 @@ constexpr int kStatStride = 16;  // u64 per shard (128 B)
 // traces the children: the latency-bound deep levels overlap with shading work.
 // packet_mask selects wave-packet traversal per kernel and level class
 enum : int { kPacketClosest0 = 1, kPacketClosestN = 2, kPacketShadow0 = 4, kPacketShadowN = 8 };
-hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
-                          const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
-                          hipStream_t stream, int packet_mask);
+// n: the level's ray count (level 0), or with n_dev (the previous level's child counter,
+// read on the device) an upper bound used only to size the grid.
+hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
+                          int remaining_depth, const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr,
+                          unsigned long long* stats, hipStream_t stream, int packet_mask);
 // Shading of one or more levels in one launch (the deep levels are shaded together once
 // the closest-hit chain has finished).  Items of each level start on a wave boundary so
 // that every wave belongs to one level.  levels_dev: device copy of the RayLevel records.

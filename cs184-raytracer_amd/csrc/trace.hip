@@ -12,6 +12,7 @@
 // then colours are reduced bottom-up (k_reduce) in the reference's addition order:
 // colour = (local + refraction) + reflection * kr (scene.cpp:127,134).
 // Device arithmetic: see intersect.h; pow is glibc's (glibc_pow.h).
+#include <algorithm>
 #include "trace.h"
 #include "glibc_pow.h"
 #include "intersect.h"
@@ -154,19 +155,15 @@ __device__ __forceinline__ Slots block_append2(bool a, bool b0, bool b1, int32_t
 // Closest hit (castRay, scene.cpp:142-167) + the bounce decisions of scene.cpp:110-136:
 // the children's rays and the reflective weight depend only on the hit, not on the
 // shading, so they are spawned here and level L+1 can be traced while level L is shaded.
+// One item (thread t of the level's index space) of k_closest; every thread of the block
+// calls it (block_append2 synchronises the block).
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScene S, FrameGeometry fg, int level,
-                                                                      int64_t n, int remaining, RayLevel cur,
-                                                                      RayLevel next, DeviceCounters* ctr,
-                                                                      unsigned long long* stats) {
-	__shared__ AppendLds append_lds;
-	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackWords * kStackDepth * kBlock];
-	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	const int64_t t = xcd_block() * kBlock + threadIdx.x;
+__device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
+                                             int remaining, const RayLevel& cur, const RayLevel& next,
+                                             DeviceCounters* ctr, unsigned long long* stats, int64_t t,
+                                             AppendLds& append_lds, int32_t* stack) {
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
-	// the next level's counts start at zero (its k_closest appends to them)
-	if (remaining > 0 && blockIdx.x == 0 && threadIdx.x == 0) next.counts[0] = next.counts[1] = 0;
 	WorkStats ws{0, 0, 0, 0, 0};
 	bool hit = false;
 	int gi = -1;
@@ -274,6 +271,28 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScen
 	cur.hit_list[slot.a] = (int32_t)i;
 }
 
+// Level 0: one thread per pixel (n_dev null, exact grid).  Deeper levels are launched
+// before the host knows their size: the ray count is read from the previous level's
+// child counter (n_dev) and a fixed grid strides over it, so each level is queued behind
+// the previous one without a host round trip.
+template <bool kPacket>
+__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScene S, FrameGeometry fg, int level,
+                                                                      int64_t n_host, const int32_t* n_dev,
+                                                                      int remaining, RayLevel cur, RayLevel next,
+                                                                      DeviceCounters* ctr,
+                                                                      unsigned long long* stats) {
+	__shared__ AppendLds append_lds;
+	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	// the next level's counts start at zero (its k_closest appends to them)
+	if (remaining > 0 && blockIdx.x == 0 && threadIdx.x == 0) next.counts[0] = next.counts[1] = 0;
+	const int64_t n = n_dev ? static_cast<int64_t>(*n_dev) : n_host;
+	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride)
+		closest_item<kPacket>(S, fg, level, n, remaining, cur, next, ctr, stats, base + threadIdx.x, append_lds, stack);
+}
+
 // Level of item t of a batch (wave-uniform: every level's items start on a wave boundary)
 struct BatchItem {
 	int32_t level;
@@ -294,7 +313,7 @@ template <bool kPacket>
 __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
-	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackWords * kStackDepth * kBlock];
+	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
 	const int64_t tg = xcd_block() * kBlock + threadIdx.x;
 	const BatchItem it = batch_item(B, B.shadow_begin, tg);
@@ -469,21 +488,26 @@ __global__ void k_selftest(int op, const double* x, const double* y, double* out
 }
 
 inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
+// grid of the stride loops: 8 blocks (16 waves) per CU, 4 waves per SIMD
+constexpr int64_t kStrideBlocks = 256 * 8;
 
 }  // namespace
 
-hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, int remaining_depth,
-                          const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr, unsigned long long* stats,
-                          hipStream_t stream, int packet_mask) {
+hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
+                          int remaining_depth, const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr,
+                          unsigned long long* stats, hipStream_t stream, int packet_mask) {
 	if (n <= 0) return hipSuccess;
-	if (packet_mask & (level == 0 ? kPacketClosest0 : kPacketClosestN)) {
-		const int64_t threads = level == 0 ? tile_threads(n, fg.width) : n;
-		hipLaunchKernelGGL(k_closest<true>, dim3(grid_for(threads, kBlock)), dim3(kBlock), 0, stream, s, fg, level, n,
+	const bool packet = packet_mask & (level == 0 ? kPacketClosest0 : kPacketClosestN);
+	const int64_t threads = (level == 0 && packet) ? tile_threads(n, fg.width) : n;
+	// with a device-side count, n is an upper bound: a grid of at most kStrideBlocks
+	const unsigned grid = n_dev ? (unsigned)std::min<int64_t>(grid_for(threads, kBlock), kStrideBlocks)
+	                            : grid_for(threads, kBlock);
+	if (packet)
+		hipLaunchKernelGGL(k_closest<true>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
+		                   cur, next, ctr, stats);
+	else
+		hipLaunchKernelGGL(k_closest<false>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev,
 		                   remaining_depth, cur, next, ctr, stats);
-	} else {
-		hipLaunchKernelGGL(k_closest<false>, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, stream, s, fg, level, n,
-		                   remaining_depth, cur, next, ctr, stats);
-	}
 	return hipGetLastError();
 }
 
