@@ -7,9 +7,12 @@ mirror spheres), 1920x1080, --bdepth 4.  A step renders frames of that scene thr
 the C-ABI (librtamd.so); rays = traceRay calls (primary + reflection + refraction) +
 shadow rays, counted by the kernels and equal to the reference's counts.
 
-Multi-GPU (torchrun, one rank per GPU, RCCL): every frame is row-interleaved over all
-ranks (row r -> rank r mod N) and its RGB8 rows are gathered to rank 0 over xGMI; a
-step renders N frames, so per-GPU work is fixed (weak scaling).
+Multi-GPU (torchrun, one rank per GPU, RCCL): a step renders a batch of N frames, each
+row-interleaved over all N ranks and assembled on rank 0 by an RCCL gather of its RGB8
+rows over xGMI (rtamd.dist.gather_batch).  The interleave rotates with the frame (frame
+f's rows of residue k are rendered by rank (k - f) mod N), so each rank renders every row
+once per step in ONE render call: per-GPU work is one frame per step (weak scaling) and
+each GPU pays the per-call latency of the level chain once per step, not once per frame.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3_bunny_1920x1080_bd4]
 """
@@ -36,6 +39,8 @@ NODE_FLOPS, TRI_FLOPS, CAND_FLOPS, SPHERE_FLOPS = 56, 38, 67, 98
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks on fewer GPUs)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C3_bunny_1920x1080_bd4")
@@ -103,22 +108,27 @@ def main():
     import rtamd
     from cases import CONFIGS, SCENES, option_kwargs
 
+    if a.backend == "gloo":
+        local = local % torch.cuda.device_count()  # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     scene_rel, W, H, flags = CONFIGS[a.config]
     kw = option_kwargs(flags)
     scene = os.path.join(SCENES, scene_rel)
     s = rtamd.load_scene(scene, device=local)
     s.upload()
-    n_local = len(range(rank, H, world))
     n_max = -(-H // world)
-    out = torch.empty((n_local, W, 3), dtype=torch.float64, device="cuda")
-    out8 = torch.zeros((n_max, W, 3), dtype=torch.uint8, device="cuda")
-    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rank, H, world)
+    out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    out8 = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)  # every row, once per step
     stream = torch.cuda.current_stream().cuda_stream
-    gather = [torch.empty_like(out8) for _ in range(world)] if rank == 0 and world > 1 else None
-    frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    gather = [torch.empty((n_max, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
+        if rank == 0 and world > 1 else None
+    frames = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] if rank == 0 else None
     from rtamd import dist as rd
 
     totals = {"rays": 0, "trace_rays": 0, "ms": [0.0, 0.0, 0.0], "launches": [0, 0, 0], "bytes": [0, 0, 0],
@@ -126,26 +136,27 @@ def main():
     work = {}
 
     def step(record):
-        for _ in range(world):  # N frames per step: per-GPU work fixed (weak scaling)
-            st = s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)
-            rd.gather_rows(out8, H, dst=0, out=frame, bufs=gather)  # RCCL gather of RGB8 rows
-            if record:
-                totals["rays"] += st.trace_rays + st.shadow_rays
-                totals["trace_rays"] += st.trace_rays
-                for k in range(3):
-                    totals["ms"][k] += st.stage_ms[k]
-                    totals["launches"][k] += st.stage_launches[k]
-                # SURVEY.md §8d algorithmic bytes, attributed to the kernel that moves them
-                for k, nrays in ((0, st.trace_rays), (1, st.shadow_rays)):
-                    totals["bytes"][k] += (nrays * RAY_IO_BYTES + st.stage_node_visits[k] * NODE_BYTES +
-                                           st.stage_tri_tests[k] * TRI_BYTES + st.stage_candidates[k] * NRM_BYTES)
-                    totals["flops"][k] += (st.stage_node_visits[k] * NODE_FLOPS + st.stage_tri_tests[k] * TRI_FLOPS +
-                                           st.stage_candidates[k] * CAND_FLOPS + st.stage_sphere_tests[k] * SPHERE_FLOPS)
-                totals["bytes"][2] += st.pixels * PIXEL_BYTES
-                work.update({"trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
-                             "node_visits": list(st.stage_node_visits), "tri_tests": list(st.stage_tri_tests),
-                             "candidates": list(st.stage_candidates), "sphere_tests": list(st.stage_sphere_tests),
-                             "bvh_traversals": list(st.stage_bvh_traversals)})
+        # N frames per step (weak scaling): this rank's rows of all N frames in one call,
+        # then one RCCL gather of RGB8 rows per frame
+        st = s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)
+        rd.gather_batch(out8, H, dst=0, frames=frames, bufs=gather)
+        if record:
+            totals["rays"] += st.trace_rays + st.shadow_rays
+            totals["trace_rays"] += st.trace_rays
+            for k in range(3):
+                totals["ms"][k] += st.stage_ms[k]
+                totals["launches"][k] += st.stage_launches[k]
+            # SURVEY.md §8d algorithmic bytes, attributed to the kernel that moves them
+            for k, nrays in ((0, st.trace_rays), (1, st.shadow_rays)):
+                totals["bytes"][k] += (nrays * RAY_IO_BYTES + st.stage_node_visits[k] * NODE_BYTES +
+                                       st.stage_tri_tests[k] * TRI_BYTES + st.stage_candidates[k] * NRM_BYTES)
+                totals["flops"][k] += (st.stage_node_visits[k] * NODE_FLOPS + st.stage_tri_tests[k] * TRI_FLOPS +
+                                       st.stage_candidates[k] * CAND_FLOPS + st.stage_sphere_tests[k] * SPHERE_FLOPS)
+            totals["bytes"][2] += st.pixels * PIXEL_BYTES
+            work.update({"trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
+                         "node_visits": list(st.stage_node_visits), "tri_tests": list(st.stage_tri_tests),
+                         "candidates": list(st.stage_candidates), "sphere_tests": list(st.stage_sphere_tests),
+                         "bvh_traversals": list(st.stage_bvh_traversals)})
 
     for _ in range(a.warmup):
         step(False)
@@ -193,7 +204,8 @@ def main():
             "config": {"workload": a.config, "scene": scene_rel, "width": W, "height": H,
                        "bounce_depth": kw["bdepth"], "frames_per_step": world, "rays_per_frame": int(rays / a.steps / world),
                        "ms_per_frame": round(elapsed / a.steps / world * 1e3, 3),
-                       "parallelism": f"row-interleaved x{world}, RCCL gather of RGB8 rows" if world > 1 else "1 GPU"},
+                       "parallelism": f"{world} frames/step, each row-interleaved x{world} (rotated), RCCL gather of RGB8 rows"
+                       if world > 1 else "1 GPU"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": names[dom], "avg_launch_ms": round(kms / launches, 4) if launches else None,

@@ -19,9 +19,10 @@ import torch
 import torch.distributed as dist
 
 
-def rank_rows(height: int, rank: int, world: int) -> Tuple[int, int, int]:
-    """(row_begin, row_end, row_step) of this rank's rows."""
-    return rank, height, world
+def rank_rows(height: int, rank: int, world: int, shift: int = 0) -> Tuple[int, int, int]:
+    """(row_begin, row_end, row_step) of this rank's rows; with `shift`, rank r holds the
+    rows of residue (r + shift) mod world (frame `shift` of a rotated batch)."""
+    return (rank + shift) % world, height, world
 
 
 def n_rows(height: int, rank: int, world: int) -> int:
@@ -37,8 +38,9 @@ def global_max(value: float, device: torch.device) -> float:
 
 
 def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
-                out: Optional[torch.Tensor] = None, bufs: Optional[list] = None) -> Optional[torch.Tensor]:
-    """Gathers every rank's interleaved rows (n_local, W, C) into a (H, W, C) frame on `dst`."""
+                out: Optional[torch.Tensor] = None, bufs: Optional[list] = None, shift: int = 0) -> Optional[torch.Tensor]:
+    """Gathers every rank's interleaved rows (n_local, W, C) into a (H, W, C) frame on `dst`
+    (rank r holds rows (r + shift) mod world, see rank_rows)."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     if world == 1:
@@ -47,21 +49,45 @@ def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
         out.copy_(local)
         return out
     n_max = -(-height // world)
+    if not local.is_contiguous():
+        local = local.contiguous()
     if local.shape[0] != n_max:
         pad = torch.zeros((n_max,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         pad[: local.shape[0]] = local
         local = pad
+    staged = local.is_cuda and dist.get_backend() == "gloo"  # gloo gathers host tensors
+    if staged:
+        local = local.cpu()
     if rank == dst:
-        if bufs is None:
+        if bufs is None or staged:
             bufs = [torch.empty_like(local) for _ in range(world)]
         dist.gather(local, bufs, dst=dst)
         if out is None:
             out = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         for r in range(world):
-            out[r::world] = bufs[r][: n_rows(height, r, world)]
+            k = (r + shift) % world
+            out[k::world] = bufs[r][: n_rows(height, k, world)].to(out.device)
         return out
     dist.gather(local, None, dst=dst)
     return None
+
+
+def gather_batch(full: torch.Tensor, height: int, dst: int = 0, frames: Optional[list] = None,
+                 bufs: Optional[list] = None) -> Optional[list]:
+    """A batch of `world` frames of one scene, each row-interleaved over all ranks.
+
+    Frame f's rows of residue k mod world are rendered by rank (k - f) mod world, so over
+    the batch every rank renders each row once: `full` (H, W, C) is this rank's single
+    render of all rows, and frame f is assembled on `dst` from the rows every rank holds
+    for it (one gather per frame).  Returns the frames on `dst`."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    outs = []
+    for f in range(world):
+        first = (rank + f) % world
+        out = frames[f] if frames is not None and rank == dst else None
+        outs.append(gather_rows(full[first::world], height, dst, out=out, bufs=bufs, shift=f))
+    return outs if rank == dst else None
 
 
 def render_frame(render_rows: Callable[[Tuple[int, int, int]], Tuple[torch.Tensor, float]], height: int,

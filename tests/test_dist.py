@@ -58,3 +58,40 @@ def test_partitioned_frame_equals_single_render(oracle, scene, io, world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert np.array_equal(got, want)
+
+
+def _batch_worker(rank, world, port, scene, w, h, bdepth, q):
+    import torch.distributed as dist
+    import pyoracle
+    from rtamd import dist as rd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        img, _ = pyoracle.render(scene, w, h, bdepth=bdepth, threads=2)
+        full = torch.from_numpy(img)
+        frames = rd.gather_batch(full, h)
+        if rank == 0:
+            q.put([fr.numpy() for fr in frames])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rotated_batch_assembles_every_frame(oracle, world):
+    """bench.py's N-frame step: frame f's rows come from all ranks (rotated interleave)."""
+    w, h, bdepth = 29, 17, 3
+    path = os.path.join(SCENES, "excess_inputs/bunny.rti")
+    want, _ = oracle.render(path, w, h, bdepth=bdepth)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_worker, args=(r, world, port, path, w, h, bdepth, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(got) == world
+    for fr in got:
+        assert np.array_equal(fr, want)
