@@ -123,7 +123,10 @@ def main():
     s.upload()
     n_max = -(-H // world)
     out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
-    out8 = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+    # RGB8 output double-buffered: the gathers of step i (side stream) overlap the render of i+1
+    out8s = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    gathered = [None, None]
+    comm = torch.cuda.Stream() if world > 1 else torch.cuda.current_stream()
     prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)  # every row, once per step
     stream = torch.cuda.current_stream().cuda_stream
     gather = [torch.empty((n_max, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
@@ -135,11 +138,23 @@ def main():
               "flops": [0, 0, 0]}
     work = {}
 
+    n_steps = [0]
+
     def step(record):
         # N frames per step (weak scaling): this rank's rows of all N frames in one call,
-        # then one RCCL gather of RGB8 rows per frame
-        st = s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)
-        rd.gather_batch(out8, H, dst=0, frames=frames, bufs=gather)
+        # then one RCCL gather of RGB8 rows per frame, on a side stream
+        k = n_steps[0] % 2
+        n_steps[0] += 1
+        if gathered[k] is not None:  # the gathers that read this buffer two steps ago
+            torch.cuda.current_stream().wait_event(gathered[k])
+        st = s.render_device(prm, out.data_ptr(), out8s[k].data_ptr(), stream)
+        rendered = torch.cuda.Event()
+        rendered.record()
+        with torch.cuda.stream(comm):
+            comm.wait_event(rendered)
+            rd.gather_batch(out8s[k], H, dst=0, frames=frames, bufs=gather)
+            gathered[k] = torch.cuda.Event()
+            gathered[k].record(comm)
         if record:
             totals["rays"] += st.trace_rays + st.shadow_rays
             totals["trace_rays"] += st.trace_rays
