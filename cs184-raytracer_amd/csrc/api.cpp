@@ -59,6 +59,7 @@ struct LevelBuffers {
 // those gaps (tools/tail_test.py: 1/8 of the C3 frame alone takes 55 % of the frame's time).
 struct Lane {
 	hipStream_t stream = nullptr;        // k_closest chain, reduce, output (high priority)
+	hipStream_t readback = nullptr;      // level counts -> host, off the chain's stream
 	// k_shadow + k_shade of level L < direct_levels on shade[L % 3]; the small deep levels
 	// are shaded in batches on shade[3] once the chain has finished
 	hipStream_t shade[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -92,9 +93,9 @@ struct rt_scene {
 	rt_scene_info info{};
 	std::vector<std::unique_ptr<Lane>> lanes;
 	rtamd::DeviceCounters* ctr = nullptr;        // device
-	rtamd::DeviceCounters* ctr_host = nullptr;   // pinned mirror
 	unsigned long long* stats = nullptr;         // device, kStatShards x kStatStride
-	std::vector<unsigned long long> stats_host;
+	unsigned long long* summary = nullptr;       // device, ST_COUNT + 1 (k_stats_finish)
+	unsigned long long* summary_host = nullptr;  // pinned mirror
 	double* out_dev = nullptr;                   // staging for rt_render
 	int64_t out_capacity = 0;
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
@@ -205,6 +206,7 @@ int ensure_events(Lane& ln, size_t level) {
 
 int lane_create(Lane& ln, int prio_low, int prio_high) {
 	HIP_TRY(hipStreamCreateWithPriority(&ln.stream, hipStreamNonBlocking, prio_high));
+	HIP_TRY(hipStreamCreateWithPriority(&ln.readback, hipStreamNonBlocking, prio_high));
 	for (hipStream_t& q : ln.shade) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
 	HIP_TRY(hipEventCreateWithFlags(&ln.chunk_done, hipEventDisableTiming));
 	return RT_OK;
@@ -221,6 +223,7 @@ void lane_destroy(Lane& ln) {
 	if (ln.chunk_done) (void)hipEventDestroy(ln.chunk_done);
 	for (hipStream_t q : ln.shade)
 		if (q) (void)hipStreamDestroy(q);
+	if (ln.readback) (void)hipStreamDestroy(ln.readback);
 	if (ln.stream) (void)hipStreamDestroy(ln.stream);
 }
 
@@ -254,9 +257,10 @@ struct Render {
 		                              s->packet_mask));
 		cnt.stage_launches[0]++;
 		HIP_TRY(hipEventRecord(ev[1], ln.stream));
+		HIP_TRY(hipStreamWaitEvent(ln.readback, ev[1], 0));
 		HIP_TRY(hipMemcpyAsync(ln.counts_host + 2 * L, cur.counts, 2 * sizeof(int32_t), hipMemcpyDeviceToHost,
-		                       ln.stream));
-		HIP_TRY(hipEventRecord(ev[5], ln.stream));
+		                       ln.readback));
+		HIP_TRY(hipEventRecord(ev[5], ln.readback));
 		return RT_OK;
 	}
 
@@ -480,12 +484,19 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	HIP_TRY(hipMalloc(&c, sizeof(rtamd::DeviceCounters)));
 	s->allocs.push_back(c);
 	s->ctr = static_cast<rtamd::DeviceCounters*>(c);
-	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->ctr_host), sizeof(rtamd::DeviceCounters), hipHostMallocDefault));
 	void* st = nullptr;
 	HIP_TRY(hipMalloc(&st, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
 	s->allocs.push_back(st);
 	s->stats = static_cast<unsigned long long*>(st);
-	s->stats_host.resize(rtamd::kStatShards * rtamd::kStatStride);
+	void* sm = nullptr;
+	HIP_TRY(hipMalloc(&sm, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1)));
+	s->allocs.push_back(sm);
+	s->summary = static_cast<unsigned long long*>(sm);
+	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->summary_host), sizeof(unsigned long long) * (rtamd::ST_COUNT + 1),
+	                      hipHostMallocDefault));
+	// statistics and the error word start cleared; k_stats_finish clears them after each render
+	HIP_TRY(hipMemset(s->ctr, 0, sizeof(rtamd::DeviceCounters)));
+	HIP_TRY(hipMemset(s->stats, 0, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
 	rt_scene_info& in = s->info;
 	in.n_geometries = s->ds.n_geoms;
 	for (const auto& g : fs.geoms) (g.kind == rtamd::GEOM_SPHERE ? in.n_spheres : in.n_meshes)++;
@@ -503,7 +514,7 @@ void rt_scene_destroy(rt_scene* s) {
 	for (auto& ln : s->lanes) lane_destroy(*ln);
 	for (void* p : s->allocs) (void)hipFree(p);
 	if (s->out_dev) (void)hipFree(s->out_dev);
-	if (s->ctr_host) (void)hipHostFree(s->ctr_host);
+	if (s->summary_host) (void)hipHostFree(s->summary_host);
 	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
 	delete s;
@@ -526,8 +537,6 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 	const int64_t n_rows = selected_rows(p);
 	Render R{s, p->intersection_only ? 0 : p->bounce_depth, p->intersection_only != 0, out_rgb_dev, out_rgb8_dev, W};
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
-	HIP_TRY(hipMemsetAsync(s->ctr, 0, sizeof(rtamd::DeviceCounters), caller));
-	HIP_TRY(hipMemsetAsync(s->stats, 0, sizeof(unsigned long long) * s->stats_host.size(), caller));
 	HIP_TRY(hipEventRecord(s->fork_event, caller));
 	for (auto& ln : s->lanes) HIP_TRY(hipStreamWaitEvent(ln->stream, s->fork_event, 0));
 	// chunks: at most 4 M pixels (bounds the level buffers), and enough of them for every
@@ -558,19 +567,16 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		}
 		if (!busy) break;
 	}
-	HIP_TRY(hipDeviceSynchronize());
-	HIP_TRY(hipMemcpy(s->ctr_host, s->ctr, sizeof(rtamd::DeviceCounters), hipMemcpyDeviceToHost));
-	if (s->ctr_host->error) return fail(RT_ERR_MATH, device_error_text(s->ctr_host->error));
+	// all lanes' work is complete (their events were observed): reduce the statistics on the
+	// device and read back one small summary
+	HIP_TRY(rtamd::launch_stats_finish(s->stats, s->ctr, s->summary, caller));
+	HIP_TRY(hipMemcpyAsync(s->summary_host, s->summary, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1),
+	                       hipMemcpyDeviceToHost, caller));
+	HIP_TRY(hipStreamSynchronize(caller));
+	const unsigned long long* sum = s->summary_host;
+	if (sum[rtamd::ST_COUNT]) return fail(RT_ERR_MATH, device_error_text(static_cast<int>(sum[rtamd::ST_COUNT])));
 	rt_counters& cnt = R.cnt;
 	const int io = R.io;
-	HIP_TRY(hipMemcpy(s->stats_host.data(), s->stats, sizeof(unsigned long long) * s->stats_host.size(),
-	                  hipMemcpyDeviceToHost));
-	unsigned long long sum[rtamd::ST_COUNT] = {0};
-	for (int sh = 0; sh < rtamd::kStatShards; sh++)
-		for (int k = 0; k < rtamd::ST_COUNT; k++) {
-			const unsigned long long v = s->stats_host[sh * rtamd::kStatStride + k];
-			sum[k] = (k == rtamd::ST_MAX_BITS) ? std::max(sum[k], v) : sum[k] + v;
-		}
 	cnt.shadow_rays = static_cast<int64_t>(sum[rtamd::ST_HITS]) * s->ds.n_nonambient;
 	cnt.reflect_rays = static_cast<int64_t>(sum[rtamd::ST_REFL]);
 	cnt.refract_rays = static_cast<int64_t>(sum[rtamd::ST_REFR]);

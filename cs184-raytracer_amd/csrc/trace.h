@@ -100,6 +100,11 @@ hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const Sha
 hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream);
 hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8_t* out_rgb8,
                          int32_t intersection_only, unsigned long long* stats, hipStream_t stream);
+// End of a render: summary[k] = sum over the shards of statistic k (max for ST_MAX_BITS),
+// summary[ST_COUNT] = the device error word; the shards and the error word are cleared for
+// the next render.
+hipError_t launch_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary,
+                               hipStream_t stream);
 hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uint8_t* out_rgb8, hipStream_t stream);
 hipError_t launch_selftest_math(int op, const double* x, const double* y, double* out, int64_t n, hipStream_t stream);
 

@@ -468,6 +468,22 @@ __global__ void k_output(int64_t n, RayLevel lvl0, double* out, uint8_t* out8, i
 	}
 }
 
+__global__ void k_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary) {
+	const int t = threadIdx.x;
+	if (t < ST_COUNT) {
+		unsigned long long acc = 0;
+		for (int sh = 0; sh < kStatShards; sh++) {
+			const unsigned long long v = stats[sh * kStatStride + t];
+			acc = (t == ST_MAX_BITS) ? (v > acc ? v : acc) : acc + v;
+		}
+		summary[t] = acc;
+	}
+	if (t == ST_COUNT) summary[t] = static_cast<unsigned long long>(ctr->error);
+	__syncthreads();
+	for (int k = t; k < kStatShards * kStatStride; k += blockDim.x) stats[k] = 0;
+	if (t == 0) ctr->error = 0;
+}
+
 __global__ void k_normalize(int64_t n_values, double* rgb, double rcp, uint8_t* out8) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n_values) return;
@@ -543,6 +559,12 @@ hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8
                          unsigned long long* stats, hipStream_t stream) {
 	if (n <= 0) return hipSuccess;
 	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, lvl0, out_rgb, out_rgb8, io, stats);
+	return hipGetLastError();
+}
+
+hipError_t launch_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary,
+                               hipStream_t stream) {
+	hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(256), 0, stream, stats, ctr, summary);
 	return hipGetLastError();
 }
 
