@@ -171,7 +171,8 @@ def main():
             work.update({"trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
                          "node_visits": list(st.stage_node_visits), "tri_tests": list(st.stage_tri_tests),
                          "candidates": list(st.stage_candidates), "sphere_tests": list(st.stage_sphere_tests),
-                         "bvh_traversals": list(st.stage_bvh_traversals)})
+                         "bvh_traversals": list(st.stage_bvh_traversals),
+                         "max_node_visits_per_ray": list(st.stage_max_node_visits)})
 
     for _ in range(a.warmup):
         step(False)

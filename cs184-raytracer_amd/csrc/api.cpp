@@ -587,6 +587,7 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		cnt.stage_candidates[k] = static_cast<int64_t>(sum[b + 2]);
 		cnt.stage_sphere_tests[k] = static_cast<int64_t>(sum[b + 3]);
 		cnt.stage_bvh_traversals[k] = static_cast<int64_t>(sum[k ? rtamd::ST_ENTRIES1 : rtamd::ST_ENTRIES0]);
+		cnt.stage_max_node_visits[k] = static_cast<int64_t>(sum[k ? rtamd::ST_MAXNODES1 : rtamd::ST_MAXNODES0]);
 		cnt.node_visits += cnt.stage_node_visits[k];
 		cnt.tri_tests += cnt.stage_tri_tests[k];
 		cnt.candidates += cnt.stage_candidates[k];

@@ -66,6 +66,7 @@ enum StatSlot : int {
 	ST_NODES0, ST_TRIS0, ST_CANDS0, ST_SPHERES0,   // k_closest
 	ST_NODES1, ST_TRIS1, ST_CANDS1, ST_SPHERES1,   // k_shadow
 	ST_ENTRIES0, ST_ENTRIES1,                      // LBVH traversals started
+	ST_MAXNODES0, ST_MAXNODES1,                    // most node visits of one ray (max)
 	ST_COUNT
 };
 constexpr int kStatStride = 16;  // u64 per shard (128 B)

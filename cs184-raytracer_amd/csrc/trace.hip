@@ -104,9 +104,14 @@ __device__ __forceinline__ unsigned long long* shard(unsigned long long* stats) 
 
 __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long long* stats, int stage) {
 	unsigned long long w[5] = {ws.nodes, ws.tris, ws.cands, ws.spheres, ws.bvh_entries};
+	unsigned long long wmax = ws.nodes;
 #pragma unroll
 	for (int k = 0; k < 5; k++)
 		for (int o = 32; o > 0; o >>= 1) w[k] += __shfl_xor(w[k], o);
+	for (int o = 32; o > 0; o >>= 1) {
+		const unsigned long long v = __shfl_xor(wmax, o);
+		wmax = v > wmax ? v : wmax;
+	}
 	if (__lane_id() == 0) {
 		unsigned long long* sh = shard(stats);
 		const int base = stage ? ST_NODES1 : ST_NODES0;
@@ -114,6 +119,7 @@ __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long l
 		for (int k = 0; k < 4; k++)
 			if (w[k]) atomicAdd(sh + base + k, w[k]);
 		if (w[4]) atomicAdd(sh + (stage ? ST_ENTRIES1 : ST_ENTRIES0), w[4]);
+		if (wmax) atomicMax(sh + (stage ? ST_MAXNODES1 : ST_MAXNODES0), wmax);
 	}
 }
 
@@ -474,7 +480,7 @@ __global__ void k_stats_finish(unsigned long long* stats, DeviceCounters* ctr, u
 		unsigned long long acc = 0;
 		for (int sh = 0; sh < kStatShards; sh++) {
 			const unsigned long long v = stats[sh * kStatStride + t];
-			acc = (t == ST_MAX_BITS) ? (v > acc ? v : acc) : acc + v;
+			acc = (t == ST_MAX_BITS || t == ST_MAXNODES0 || t == ST_MAXNODES1) ? (v > acc ? v : acc) : acc + v;
 		}
 		summary[t] = acc;
 	}

@@ -102,6 +102,7 @@ typedef struct rt_counters {
 	int32_t stage_launches[3];
 	int64_t stage_node_visits[2], stage_tri_tests[2], stage_candidates[2], stage_sphere_tests[2];
 	int64_t stage_bvh_traversals[2];   /* mesh LBVH traversals started (after the mesh gate) */
+	int64_t stage_max_node_visits[2];  /* most LBVH nodes one ray visited (all meshes)       */
 } rt_counters;
 
 /* Scene::renderScene into a caller-owned host buffer of n_rows*W*3 doubles
