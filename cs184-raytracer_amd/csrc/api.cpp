@@ -154,6 +154,7 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	L.lv.inside = reinterpret_cast<uint8_t*>(take(n));
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
+	HIP_TRY(hipMemset(L.lv.counts, 0, 2 * sizeof(int32_t)));
 	L.lv.capacity = capacity;
 	return RT_OK;
 }
@@ -250,8 +251,8 @@ struct Render {
 		const auto& ev = ln.level_events[L];
 		const rtamd::RayLevel& cur = ln.levels[L].lv;
 		const rtamd::RayLevel& next = remaining > 0 ? ln.levels[L + 1].lv : cur;
-		// level 0's counts are cleared here, deeper ones by the previous level's k_closest
-		if (L == 0) HIP_TRY(hipMemsetAsync(cur.counts, 0, 2 * sizeof(int32_t), ln.stream));
+		// counts start at zero: level 0's are cleared at allocation and by the previous
+		// chunk's k_output, deeper ones by the previous level's k_closest
 		HIP_TRY(hipEventRecord(ev[0], ln.stream));
 		HIP_TRY(rtamd::launch_closest(s->ds, ln.fg, L, n, n_dev, remaining, cur, next, s->ctr, s->stats, ln.stream,
 		                              s->packet_mask));

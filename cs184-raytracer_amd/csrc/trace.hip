@@ -447,6 +447,8 @@ __device__ __forceinline__ uint8_t to_u8(double v) {
 
 __global__ void k_output(int64_t n, RayLevel lvl0, double* out, uint8_t* out8, int32_t io, unsigned long long* stats) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	// level 0's counts were read back; clear them for the lane's next chunk
+	if (i == 0) lvl0.counts[0] = lvl0.counts[1] = 0;
 	double v[3] = {0, 0, 0};
 	if (i < n) {
 		v[0] = lvl0.cr[i];
@@ -474,20 +476,31 @@ __global__ void k_output(int64_t n, RayLevel lvl0, double* out, uint8_t* out8, i
 	}
 }
 
+// one block of kStatShards threads: thread t owns shard t; tree reduction in LDS
 __global__ void k_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary) {
+	__shared__ unsigned long long red[kStatShards][ST_COUNT + 1];
 	const int t = threadIdx.x;
-	if (t < ST_COUNT) {
-		unsigned long long acc = 0;
-		for (int sh = 0; sh < kStatShards; sh++) {
-			const unsigned long long v = stats[sh * kStatStride + t];
-			acc = (t == ST_MAX_BITS || t == ST_MAXNODES0 || t == ST_MAXNODES1) ? (v > acc ? v : acc) : acc + v;
-		}
-		summary[t] = acc;
+	auto is_max = [](int k) { return k == ST_MAX_BITS || k == ST_MAXNODES0 || k == ST_MAXNODES1; };
+#pragma unroll
+	for (int k = 0; k < ST_COUNT; k++) {
+		red[t][k] = stats[t * kStatStride + k];
+		stats[t * kStatStride + k] = 0;
 	}
-	if (t == ST_COUNT) summary[t] = static_cast<unsigned long long>(ctr->error);
 	__syncthreads();
-	for (int k = t; k < kStatShards * kStatStride; k += blockDim.x) stats[k] = 0;
-	if (t == 0) ctr->error = 0;
+	for (int half = kStatShards / 2; half > 0; half >>= 1) {
+		if (t < half)
+#pragma unroll
+			for (int k = 0; k < ST_COUNT; k++) {
+				const unsigned long long a = red[t][k], b = red[t + half][k];
+				red[t][k] = is_max(k) ? (a > b ? a : b) : a + b;
+			}
+		__syncthreads();
+	}
+	if (t < ST_COUNT) summary[t] = red[0][t];
+	if (t == ST_COUNT) {
+		summary[t] = static_cast<unsigned long long>(ctr->error);
+		ctr->error = 0;
+	}
 }
 
 __global__ void k_normalize(int64_t n_values, double* rgb, double rcp, uint8_t* out8) {
@@ -570,7 +583,7 @@ hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8
 
 hipError_t launch_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary,
                                hipStream_t stream) {
-	hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(256), 0, stream, stats, ctr, summary);
+	hipLaunchKernelGGL(k_stats_finish, dim3(1), dim3(kStatShards), 0, stream, stats, ctr, summary);
 	return hipGetLastError();
 }
 
