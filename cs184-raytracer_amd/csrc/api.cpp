@@ -250,11 +250,10 @@ struct Render {
 		if ((rc = ensure_events(ln, L))) return rc;
 		const auto& ev = ln.level_events[L];
 		const rtamd::RayLevel& cur = ln.levels[L].lv;
-		const rtamd::RayLevel& next = remaining > 0 ? ln.levels[L + 1].lv : cur;
 		// counts start at zero: level 0's are cleared at allocation and by the previous
 		// chunk's k_output, deeper ones by the previous level's k_closest
 		HIP_TRY(hipEventRecord(ev[0], ln.stream));
-		HIP_TRY(rtamd::launch_closest(s->ds, ln.fg, L, n, n_dev, remaining, cur, next, s->ctr, s->stats, ln.stream,
+		HIP_TRY(rtamd::launch_closest(s->ds, ln.fg, L, n, n_dev, remaining, ln.levels_dev, s->ctr, s->stats, ln.stream,
 		                              s->packet_mask));
 		cnt.stage_launches[0]++;
 		HIP_TRY(hipEventRecord(ev[1], ln.stream));

@@ -79,9 +79,10 @@ constexpr int kStatStride = 16;  // u64 per shard (128 B)
 // packet_mask selects wave-packet traversal per kernel and level class
 enum : int { kPacketClosest0 = 1, kPacketClosestN = 2, kPacketShadow0 = 4, kPacketShadowN = 8 };
 // n: the level's ray count (level 0), or with n_dev (the previous level's child counter,
-// read on the device) an upper bound used only to size the grid.
+// read on the device) an upper bound used only to size the grid.  levels_dev: the device
+// copy of the RayLevel records (level and level + 1 must be current).
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
-                          int remaining_depth, const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr,
+                          int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
                           unsigned long long* stats, hipStream_t stream, int packet_mask);
 // Shading of one or more levels in one launch (the deep levels are shaded together once
 // the closest-hit chain has finished).  Items of each level start on a wave boundary so

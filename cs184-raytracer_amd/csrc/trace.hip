@@ -24,15 +24,23 @@ using namespace dev;
 
 constexpr int kShadeBlock = 512;
 
-// Occupancy target of the traversal kernels (waves per SIMD); 0 = compiler's choice.
+// Occupancy targets of the traversal kernels (waves per SIMD); 0 = compiler's choice.
 // 4 (<= 128 VGPRs, a few spills) measured 3 % faster than the compiler's 3 on C3.
 #ifndef RT_TRAVERSAL_WAVES
 #define RT_TRAVERSAL_WAVES 4
+#endif
+#ifndef RT_CLOSEST_WAVES
+#define RT_CLOSEST_WAVES RT_TRAVERSAL_WAVES
 #endif
 #if RT_TRAVERSAL_WAVES > 0
 #define RT_TRAVERSAL_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRAVERSAL_WAVES)))
 #else
 #define RT_TRAVERSAL_ATTR
+#endif
+#if RT_CLOSEST_WAVES > 0
+#define RT_CLOSEST_ATTR __attribute__((amdgpu_waves_per_eu(RT_CLOSEST_WAVES)))
+#else
+#define RT_CLOSEST_ATTR
 #endif  // 8 waves: one child-allocation atomic per 512 rays
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
@@ -163,9 +171,9 @@ __device__ __forceinline__ Slots block_append2(bool a, bool b0, bool b1, int32_t
 // shading, so they are spawned here and level L+1 can be traced while level L is shaded.
 // One item (thread t of the level's index space) of k_closest; every thread of the block
 // calls it (block_append2 synchronises the block).
-template <bool kPacket>
+template <bool kPacket, typename LV>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
-                                             int remaining, const RayLevel& cur, const RayLevel& next,
+                                             int remaining, const LV& cur, const LV& next,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
                                              AppendLds& append_lds, int32_t* stack) {
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
@@ -282,14 +290,17 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 // child counter (n_dev) and a fixed grid strides over it, so each level is queued behind
 // the previous one without a host round trip.
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_closest(DeviceScene S, FrameGeometry fg, int level,
+__global__ void __launch_bounds__(kBlock) RT_CLOSEST_ATTR k_closest(DeviceScene S, FrameGeometry fg, int level,
                                                                       int64_t n_host, const int32_t* n_dev,
-                                                                      int remaining, RayLevel cur, RayLevel next,
+                                                                      int remaining, const RayLevel* levels,
                                                                       DeviceCounters* ctr,
                                                                       unsigned long long* stats) {
 	__shared__ AppendLds append_lds;
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	// level records read through the constant address space (scalar loads at their uses)
+	const auto& cur = *uniform_ptr(levels + level);
+	const auto& next = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
 	// the next level's counts start at zero (its k_closest appends to them)
 	if (remaining > 0 && blockIdx.x == 0 && threadIdx.x == 0) next.counts[0] = next.counts[1] = 0;
 	const int64_t n = n_dev ? static_cast<int64_t>(*n_dev) : n_host;
@@ -529,7 +540,7 @@ constexpr int64_t kStrideBlocks = 256 * 8;
 }  // namespace
 
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
-                          int remaining_depth, const RayLevel& cur, const RayLevel& next, DeviceCounters* ctr,
+                          int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
                           unsigned long long* stats, hipStream_t stream, int packet_mask) {
 	if (n <= 0) return hipSuccess;
 	const bool packet = packet_mask & (level == 0 ? kPacketClosest0 : kPacketClosestN);
@@ -539,10 +550,10 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 	                            : grid_for(threads, kBlock);
 	if (packet)
 		hipLaunchKernelGGL(k_closest<true>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
-		                   cur, next, ctr, stats);
+		                   levels_dev, ctr, stats);
 	else
 		hipLaunchKernelGGL(k_closest<false>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev,
-		                   remaining_depth, cur, next, ctr, stats);
+		                   remaining_depth, levels_dev, ctr, stats);
 	return hipGetLastError();
 }
 
