@@ -121,9 +121,17 @@ struct MeshBest {
 	double dist;
 	int32_t face;   // global face index, -1 = none
 	int32_t id;     // reference order within the mesh (tie-break)
-	double a, b;
-	V3 n;
+	double a, b;    // barycentrics of the best face; its normal is interpolated again at the end
 };
+
+// Interpolated normal ((1 - a - b) n0 + a n1) + b n2 of face f (geometry.cpp:117-119)
+template <bool kUniform = false>
+__device__ __forceinline__ V3 face_normal(const DeviceScene& S, int32_t f, double a, double b) {
+	const auto N = scene_ptr<kUniform>(S.fnrm) + f;
+	const double w0 = (1.0 - a) - b;
+	const V3 n0 = load3(N->n0), n1 = load3(N->n1), n2 = load3(N->n2);
+	return mk((w0 * n0.x + a * n1.x) + b * n2.x, (w0 * n0.y + a * n1.y) + b * n2.y, (w0 * n0.z + a * n1.z) + b * n2.z);
+}
 
 // Exact pre-tests on q = num / den (den != 0): true only when the correctly rounded
 // quotient certainly satisfies the predicate, so skipping the division cannot change a
@@ -169,10 +177,7 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	const int32_t id = scene_ptr<kUniform>(S.fid)[f];
 	if (!(dist < best.dist || (dist == best.dist && id < best.id))) return false;
 	ws.cands++;
-	const auto N = scene_ptr<kUniform>(S.fnrm) + f;
-	const double w0 = (1.0 - a) - b;
-	const V3 n0 = load3(N->n0), n1 = load3(N->n1), n2 = load3(N->n2);
-	const V3 tn = mk((w0 * n0.x + a * n1.x) + b * n2.x, (w0 * n0.y + a * n1.y) + b * n2.y, (w0 * n0.z + a * n1.z) + b * n2.z);
+	const V3 tn = face_normal<kUniform>(S, f, a, b);
 	const bool front = dot4z(tn, d) < 0;
 	if (!front ^ reverse) return false;
 	best.dist = dist;
@@ -180,7 +185,6 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	best.id = id;
 	best.a = a;
 	best.b = b;
-	best.n = tn;
 	return kAnyHit && dist < any_limit;
 }
 
@@ -287,7 +291,7 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 	// face.points_[0] + vec4dFrom3d(a * va + b * vb)
 	Po = mk(p0.x + (best.a * va.x + best.b * vb.x), p0.y + (best.a * va.y + best.b * vb.y),
 	        p0.z + (best.a * va.z + best.b * vb.z));
-	No = best.n;
+	No = face_normal(S, best.face, best.a, best.b);
 	return true;
 }
 
@@ -493,7 +497,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	Po = mk(p0.x + (best.a * va.x + best.b * vb.x), p0.y + (best.a * va.y + best.b * vb.y),
 	        p0.z + (best.a * va.z + best.b * vb.z));
-	No = best.n;
+	No = face_normal(S, best.face, best.a, best.b);
 	return true;
 }
 
