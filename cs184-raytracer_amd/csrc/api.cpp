@@ -46,17 +46,15 @@ struct rt_builder {
 	rtamd::Scene scene;
 };
 
-
 struct LevelBuffers {
 	rtamd::RayLevel lv{};
 	void* block = nullptr;
 };
 
 // One render pipeline: its own level buffers, streams and events, tracing one chunk of
-// rows at a time.  A frame is split into chunks that several lanes trace concurrently:
-// every level of a chunk waits for the previous one (and the host reads its counts), so
-// a single chain leaves the GPU idle in its small deep levels; other lanes' chunks fill
-// those gaps (tools/tail_test.py: 1/8 of the C3 frame alone takes 55 % of the frame's time).
+// rows (<= 4 M pixels) at a time as a host-polled state machine (Render below).  Several
+// lanes can trace chunks of a frame concurrently (RTAMD_LANES); on C3 one lane is
+// fastest, because every chunk pays the level chain's latency.
 struct Lane {
 	hipStream_t stream = nullptr;        // k_closest chain, reduce, output (high priority)
 	hipStream_t readback = nullptr;      // level counts -> host, off the chain's stream
@@ -64,7 +62,8 @@ struct Lane {
 	// are shaded in batches on shade[3] once the chain has finished
 	hipStream_t shade[4] = {nullptr, nullptr, nullptr, nullptr};
 	std::vector<LevelBuffers> levels;
-	// RayLevel records of all levels for the batched shading kernels (pinned + device)
+	// RayLevel records of all levels, read by the kernels through the constant address space
+	// (pinned host copy + device copy, updated in stream order when a level is reallocated)
 	rtamd::RayLevel* levels_pinned = nullptr;
 	rtamd::RayLevel* levels_dev = nullptr;
 	size_t levels_cap = 0;
