@@ -117,6 +117,12 @@ struct WorkStats {
 	uint32_t nodes, tris, cands, spheres, bvh_entries;
 };
 
+// A mesh hit (face, barycentric a, b), or a sphere hit (face -1, ray parameter t in a)
+struct FaceHit {
+	int32_t face;
+	double a, b;
+};
+
 struct MeshBest {
 	double dist;
 	int32_t face;   // global face index, -1 = none
@@ -220,7 +226,7 @@ __device__ __forceinline__ double prune_limit(double best_dist) { return best_di
 //   like the closest-hit search restricted to dist <= prune_cap.
 template <bool kAnyHit, typename GP>
 __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
-                         double prune_cap, V3& Po, V3& No, bool& settled, double& found_dist, int32_t* stack,
+                         double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
                          DeviceCounters* ctr, WorkStats& ws) {
 	settled = false;
 	if (G->gate && !hits_bounding_box(o, d, G->bb_min, G->bb_max)) return false;
@@ -286,30 +292,52 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 	}
 	found_dist = best.dist;
 	if (best.face < 0) return false;
-	const DFaceGeo* F = S.fgeo + best.face;
-	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-	// face.points_[0] + vec4dFrom3d(a * va + b * vb)
-	Po = mk(p0.x + (best.a * va.x + best.b * vb.x), p0.y + (best.a * va.y + best.b * vb.y),
-	        p0.z + (best.a * va.z + best.b * vb.z));
-	No = face_normal(S, best.face, best.a, best.b);
+	fh = FaceHit{best.face, best.a, best.b};
 	return true;
 }
 
-// Sphere::calculateIntNormInObjSpace (geometry.cpp:47-67)
+// Sphere::calculateIntNormInObjSpace (geometry.cpp:47-67): the ray parameter t of the
+// hit (point o + t d, normal point - center)
 template <typename GP>
-__device__ __forceinline__ bool sphere_hit(GP G, V3 o, V3 d, bool reverse, V3& Po, V3& No) {
-	const V3 c = load3(G->center);
-	const V3 oc = o - c;
+__device__ __forceinline__ bool sphere_hit(GP G, V3 o, V3 d, bool reverse, double& t) {
+	const V3 oc = o - load3(G->center);
 	const double a = sq4(d);
 	const double b = 2 * dot4z(d, oc);
 	const double cc = sq4(oc) - G->rr;
 	const double disc = b * b - (4 * a) * cc;
 	if (disc < 0) return false;
-	const double t = reverse ? (-b + sqrt(disc)) / (2 * a) : (-b - sqrt(disc)) / (2 * a);
-	if (t < 0) return false;
-	Po = o + t * d;
-	No = Po - c;
-	return true;
+	t = reverse ? (-b + sqrt(disc)) / (2 * a) : (-b - sqrt(disc)) / (2 * a);
+	return t >= 0;
+}
+
+// Object-space hit point of a mesh face (face.points_[0] + vec4dFrom3d(a * va + b * vb),
+// geometry.cpp:121) or of a sphere (o + t d, t held in h.a)
+__device__ __forceinline__ V3 face_point(const DeviceScene& S, const FaceHit& h) {
+	const DFaceGeo* F = S.fgeo + h.face;
+	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	return mk(p0.x + (h.a * va.x + h.b * vb.x), p0.y + (h.a * va.y + h.b * vb.y), p0.z + (h.a * va.z + h.b * vb.z));
+}
+__device__ __forceinline__ V3 hit_point(const DeviceScene& S, const FaceHit& h, V3 oo, V3 dd) {
+	return h.face < 0 ? oo + h.a * dd : face_point(S, h);
+}
+
+// The closest-hit searches keep only (geometry, face, a, b) of the best hit so far; its
+// world point and object-space normal are recomputed once at the end with the same
+// expressions (bit-identical, fewer live registers during the traversals).
+__device__ __forceinline__ void winner_point_normal(const DeviceScene& S, int g, const FaceHit& h, V3 o, V3 d,
+                                                    V3& Pw, V3& No) {
+	const DGeom* G = S.geoms + g;
+	V3 Po;
+	if (h.face < 0) {
+		const V3 oo = xf_point(G->inv, o);
+		const V3 draw = xf_dir(G->inv, d);
+		Po = oo + h.a * div3(draw, sqrt(sq4(draw)));
+		No = Po - load3(G->center);
+	} else {
+		Po = face_point(S, h);
+		No = face_normal(S, h.face, h.a, h.b);
+	}
+	Pw = xf_point(G->fwd, Po);
 }
 
 // Every castRay transforms the ray into every geometry's object space, which throws for
@@ -331,6 +359,7 @@ __device__ __forceinline__ void check_may_raise(const DeviceScene& S, V3 d, bool
 __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, double& best_dist, int& best_geom, V3& hitP,
                             V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WorkStats& ws) {
 	bool found = false;
+	FaceHit best{-1, 0, 0};
 	const V3 winv = safe_inv(d);
 	check_may_raise(S, d, true, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
@@ -340,25 +369,25 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
 		const V3 oo = xf_point(G->inv, o);
 		const V3 dd = ray_dir(xf_dir(G->inv, d), ctr);
-		V3 Po, No;
+		FaceHit h{-1, 0, 0};
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
 			ws.spheres++;
-			hit = sphere_hit(G, oo, dd, reverse, Po, No);
+			hit = sphere_hit(G, oo, dd, reverse, h.a);
 		} else {
-			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, Po, No, settled, fd, stack, ctr, ws);
+			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 		}
 		if (!hit) continue;
-		const V3 Pw = xf_point(G->fwd, Po);
+		const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
 		const double dist = sqrt(sq4(Pw - o));
 		if (found && dist >= best_dist) continue;
 		found = true;
 		best_dist = dist;
 		best_geom = g;
-		hitP = Pw;
-		hitNobj = No;
+		best = h;
 	}
+	if (found) winner_point_normal(S, best_geom, best, o, d, hitP, hitNobj);
 	return found;
 }
 
@@ -384,30 +413,30 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 		if (is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
 		const double nrm = sqrt(sq4(draw));  // object-space length of the unit world direction
 		const V3 dd = div3(draw, nrm);
-		V3 Po, No;
+		FaceHit h{-1, 0, 0};
 		bool hit, settled = false;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
 			ws.spheres++;
-			hit = sphere_hit(G, oo, dd, reverse, Po, No);
+			hit = sphere_hit(G, oo, dd, reverse, h.a);
 		} else if (inf_light) {
-			hit = mesh_hit<true>(S, G, oo, dd, reverse, INFINITY, INFINITY, Po, No, settled, fd, stack, ctr, ws);
+			hit = mesh_hit<true>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 		} else {
 			// world distance of object-space dist t is ~ t / nrm
 			const double tl = dist_light * nrm;
 			const double cap = tl * (1.0 + 1e-7) + 1e-300;
-			hit = mesh_hit<true>(S, G, oo, dd, reverse, tl * (1.0 - 1e-7), cap, Po, No, settled, fd, stack, ctr, ws);
+			hit = mesh_hit<true>(S, G, oo, dd, reverse, tl * (1.0 - 1e-7), cap, h, settled, fd, stack, ctr, ws);
 			// No face up to `cap` was missed by the capped search, so a closest face beyond
 			// it lies beyond the light.  A closest face inside the 1e-7 band is decided
 			// exactly from the reference's own face choice (full closest-face search).
 			if (hit && !settled) {
 				if (fd > cap) continue;
-				hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, Po, No, settled, fd, stack, ctr, ws);
+				hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 			}
 		}
 		if (!hit) continue;
 		if (inf_light || settled) return true;
-		const V3 Pw = xf_point(G->fwd, Po);
+		const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
 		if (sqrt(sq4(Pw - o)) <= dist_light) return true;
 	}
 	return false;
@@ -427,7 +456,7 @@ __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 
 template <bool kAnyHit, typename GP>
 __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, bool on, double any_limit,
-                                double prune_cap, V3& Po, V3& No, bool& settled, double& found_dist,
+                                double prune_cap, FaceHit& fh, bool& settled, double& found_dist,
                                 int32_t* wstack, WorkStats& ws) {
 	settled = false;
 	if (G->gate) on = on && hits_bounding_box(o, d, G->bb_min, G->bb_max);
@@ -493,11 +522,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	}
 	found_dist = best.dist;
 	if (!on || best.face < 0) return false;
-	const DFaceGeo* F = S.fgeo + best.face;
-	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-	Po = mk(p0.x + (best.a * va.x + best.b * vb.x), p0.y + (best.a * va.y + best.b * vb.y),
-	        p0.z + (best.a * va.z + best.b * vb.z));
-	No = face_normal(S, best.face, best.a, best.b);
+	fh = FaceHit{best.face, best.a, best.b};
 	return true;
 }
 
@@ -505,6 +530,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
                                    int& best_geom, V3& hitP, V3& hitNobj, int32_t* wstack, DeviceCounters* ctr,
                                    WorkStats& ws) {
 	bool found = false;
+	FaceHit best{-1, 0, 0};
 	const V3 winv = safe_inv(d);
 	check_may_raise(S, d, on, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
@@ -516,27 +542,27 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
 		const V3 dd = div3(draw, sqrt(sq4(draw)));
-		V3 Po = mk(0, 0, 0), No = mk(0, 0, 0);
+		FaceHit h{-1, 0, 0};
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
 			if (cand) ws.spheres++;
-			hit = cand && sphere_hit(G, oo, dd, reverse, Po, No);
+			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		} else {
-			hit = mesh_hit_packet<false>(S, G, oo, dd, reverse, cand, INFINITY, INFINITY, Po, No, settled, fd, wstack, ws);
+			hit = mesh_hit_packet<false>(S, G, oo, dd, reverse, cand, INFINITY, INFINITY, h, settled, fd, wstack, ws);
 		}
 		if (hit) {
-			const V3 Pw = xf_point(G->fwd, Po);
+			const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
 			const double dist = sqrt(sq4(Pw - o));
 			if (!(found && dist >= best_dist)) {
 				found = true;
 				best_dist = dist;
 				best_geom = g;
-				hitP = Pw;
-				hitNobj = No;
+				best = h;
 			}
 		}
 	}
+	if (found) winner_point_normal(S, best_geom, best, o, d, hitP, hitNobj);
 	return found;
 }
 
@@ -558,29 +584,29 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
 		const double nrm = sqrt(sq4(draw));
 		const V3 dd = div3(draw, nrm);
-		V3 Po = mk(0, 0, 0), No = mk(0, 0, 0);
+		FaceHit h{-1, 0, 0};
 		bool hit, settled = false;
 		double fd = INFINITY;
 		if (G->kind == DGEOM_SPHERE) {
 			if (cand) ws.spheres++;
-			hit = cand && sphere_hit(G, oo, dd, reverse, Po, No);
+			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		} else {
 			const double tl = inf_light ? INFINITY : dist_light * nrm;
 			const double cap = inf_light ? INFINITY : tl * (1.0 + 1e-7) + 1e-300;
-			hit = mesh_hit_packet<true>(S, G, oo, dd, reverse, cand, inf_light ? INFINITY : tl * (1.0 - 1e-7), cap, Po,
-			                            No, settled, fd, wstack, ws);
+			hit = mesh_hit_packet<true>(S, G, oo, dd, reverse, cand, inf_light ? INFINITY : tl * (1.0 - 1e-7), cap, h,
+			                            settled, fd, wstack, ws);
 			// closest face inside the 1e-7 band around the light: the reference's exact choice
 			const bool band = cand && hit && !settled && !inf_light && fd <= cap;
 			if (cand && hit && !settled && !inf_light && fd > cap) hit = false;
 			if (wave_any(band)) {
 				bool s2;
 				double fd2;
-				V3 P2 = mk(0, 0, 0), N2 = mk(0, 0, 0);
-				const bool h2 = mesh_hit_packet<false>(S, G, oo, dd, reverse, band, INFINITY, INFINITY, P2, N2, s2, fd2,
-				                                       wstack, ws);
+				FaceHit h2{-1, 0, 0};
+				const bool hit2 = mesh_hit_packet<false>(S, G, oo, dd, reverse, band, INFINITY, INFINITY, h2, s2, fd2,
+				                                         wstack, ws);
 				if (band) {
-					hit = h2;
-					Po = P2;
+					hit = hit2;
+					h = h2;
 				}
 			}
 		}
@@ -588,7 +614,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 			if (inf_light || settled) {
 				occ = true;
 			} else {
-				const V3 Pw = xf_point(G->fwd, Po);
+				const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
 				if (sqrt(sq4(Pw - o)) <= dist_light) occ = true;
 			}
 		}
