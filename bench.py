@@ -44,6 +44,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="C3_bunny_1920x1080_bd4")
+    ap.add_argument("--frames-per-gpu", type=int, default=1,
+                    help="frames per GPU per step, pipelined over the scene's lanes (rt_render_batch_device)")
+    ap.add_argument("--latency-frames", type=int, default=5,
+                    help="single-frame renders timed after the run (wall-clock latency of one frame)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_round1.json"),
@@ -122,9 +126,10 @@ def main():
     s = rtamd.load_scene(scene, device=local)
     s.upload()
     n_max = -(-H // world)
-    out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    F = max(1, a.frames_per_gpu)
+    outs = [torch.empty((H, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
     # RGB8 output double-buffered: the gathers of step i (side stream) overlap the render of i+1
-    out8s = [torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    out8s = [[torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(F)] for _ in range(2)]
     gathered = [None, None]
     comm = torch.cuda.Stream() if world > 1 else torch.cuda.current_stream()
     prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)  # every row, once per step
@@ -141,18 +146,21 @@ def main():
     n_steps = [0]
 
     def step(record):
-        # N frames per step (weak scaling): this rank's rows of all N frames in one call,
-        # then one RCCL gather of RGB8 rows per frame, on a side stream
+        # F x N frames per step (weak scaling): F renders of every row on this rank, pipelined
+        # in one batch call; each render holds this rank's rows of N row-interleaved frames,
+        # assembled on rank 0 by one RCCL gather of RGB8 rows per frame, on a side stream
         k = n_steps[0] % 2
         n_steps[0] += 1
-        if gathered[k] is not None:  # the gathers that read this buffer two steps ago
+        if gathered[k] is not None:  # the gathers that read these buffers two steps ago
             torch.cuda.current_stream().wait_event(gathered[k])
-        st = s.render_device(prm, out.data_ptr(), out8s[k].data_ptr(), stream)
+        st = s.render_batch_device([prm] * F, [o.data_ptr() for o in outs], [o.data_ptr() for o in out8s[k]],
+                                   stream)
         rendered = torch.cuda.Event()
         rendered.record()
         with torch.cuda.stream(comm):
             comm.wait_event(rendered)
-            rd.gather_batch(out8s[k], H, dst=0, frames=frames, bufs=gather)
+            for f in range(F):
+                rd.gather_batch(out8s[k][f], H, dst=0, frames=frames, bufs=gather)
             gathered[k] = torch.cuda.Event()
             gathered[k].record(comm)
         if record:
@@ -168,10 +176,11 @@ def main():
                 totals["flops"][k] += (st.stage_node_visits[k] * NODE_FLOPS + st.stage_tri_tests[k] * TRI_FLOPS +
                                        st.stage_candidates[k] * CAND_FLOPS + st.stage_sphere_tests[k] * SPHERE_FLOPS)
             totals["bytes"][2] += st.pixels * PIXEL_BYTES
-            work.update({"trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
-                         "node_visits": list(st.stage_node_visits), "tri_tests": list(st.stage_tri_tests),
-                         "candidates": list(st.stage_candidates), "sphere_tests": list(st.stage_sphere_tests),
-                         "bvh_traversals": list(st.stage_bvh_traversals),
+            per = lambda xs: [x // F for x in xs]  # the batch's F renders do identical work
+            work.update({"trace_rays": st.trace_rays // F, "shadow_rays": st.shadow_rays // F,
+                         "node_visits": per(st.stage_node_visits), "tri_tests": per(st.stage_tri_tests),
+                         "candidates": per(st.stage_candidates), "sphere_tests": per(st.stage_sphere_tests),
+                         "bvh_traversals": per(st.stage_bvh_traversals),
                          "max_node_visits_per_ray": list(st.stage_max_node_visits)})
 
     for _ in range(a.warmup):
@@ -186,17 +195,29 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # wall-clock of ONE frame (this rank's rows, one render call, nothing else in flight)
+    lat = []
+    for _ in range(max(0, a.latency_frames)):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        s.render_device(prm, outs[0].data_ptr(), out8s[0][0].data_ptr(), stream)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t1)
+    lat = sorted(lat)[len(lat) // 2] if lat else float("nan")
     agg = torch.tensor([elapsed, float(totals["rays"])] + totals["ms"] + [float(x) for x in totals["launches"]] +
                        [float(x) for x in totals["bytes"]] + [float(x) for x in totals["flops"]] +
-                       [float(totals["trace_rays"])], dtype=torch.float64, device="cuda")
+                       [float(totals["trace_rays"]), lat], dtype=torch.float64, device="cuda")
     if world > 1:
         t_max = agg[0:1].clone()
+        l_max = agg[15:16].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        dist.all_reduce(l_max, op=dist.ReduceOp.MAX)
         dist.all_reduce(agg, op=dist.ReduceOp.SUM)
-        agg[0] = t_max[0]
+        agg[0], agg[15] = t_max[0], l_max[0]
     v = agg.tolist()
     elapsed, rays, stage_ms, stage_launches, stage_bytes = v[0], v[1], v[2:5], v[5:8], v[8:11]
-    stage_flops, trace_rays = v[11:14], v[14]
+    stage_flops, trace_rays, latency = v[11:14], v[14], v[15]
+    fps = world * F  # frames per step
     if rank == 0:
         value = rays / elapsed / 1e6
         names = ["k_closest", "k_shadow", "k_shade"]
@@ -218,10 +239,13 @@ def main():
             "vs_baseline": None, "dtype": "f64", "data": "synthetic: shipped reference scene data (bunny.obj), "
                                                         "deterministic, no RNG",
             "config": {"workload": a.config, "scene": scene_rel, "width": W, "height": H,
-                       "bounce_depth": kw["bdepth"], "frames_per_step": world, "rays_per_frame": int(rays / a.steps / world),
-                       "ms_per_frame": round(elapsed / a.steps / world * 1e3, 3),
-                       "parallelism": f"{world} frames/step, each row-interleaved x{world} (rotated), RCCL gather of RGB8 rows"
-                       if world > 1 else "1 GPU"},
+                       "bounce_depth": kw["bdepth"], "frames_per_step": fps, "frames_in_flight_per_gpu": F,
+                       "rays_per_frame": int(rays / a.steps / fps),
+                       "ms_per_frame": round(elapsed / a.steps / fps * 1e3, 3),
+                       "frame_latency_ms": round(latency * 1e3, 3),
+                       "parallelism": (f"{fps} frames/step: {F} pipelined renders per GPU, each holding its rows of "
+                                       f"{world} frames row-interleaved x{world} (rotated), RCCL gather of RGB8 rows")
+                       if world > 1 else f"1 GPU, {F} frames/step pipelined (rt_render_batch_device)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": names[dom], "avg_launch_ms": round(kms / launches, 4) if launches else None,
@@ -230,8 +254,8 @@ def main():
                          "note": "algorithmic bytes per SURVEY.md §8d (ray I/O + LBVH nodes + triangles + normals), "
                                  "mostly L2/MALL-resident scene reads; kernel times are HIP-event spans of launches "
                                  "that run concurrently with other levels' kernels; see DESIGN.md",
-                         "stages": {names[k]: {"ms_per_frame": round(stage_ms[k] / a.steps / world, 4),
-                                               "launches_per_frame": stage_launches[k] / a.steps / world,
+                         "stages": {names[k]: {"ms_per_frame": round(stage_ms[k] / a.steps / fps, 4),
+                                               "launches_per_frame": stage_launches[k] / a.steps / fps,
                                                "GBps": round(stage_bytes[k] / (stage_ms[k] * 1e-3) / 1e9, 1)
                                                if stage_ms[k] else None} for k in range(3)},
                          "work_per_frame_rank0": work},

@@ -46,6 +46,16 @@ struct rt_builder {
 	rtamd::Scene scene;
 };
 
+// One image (or row selection) of a render call: its parameters, outputs and the rows
+// not yet handed to a lane.
+struct Job {
+	const rt_render_params* p;
+	double* out_rgb_dev;
+	uint8_t* out_rgb8_dev;
+	int depth, io;
+	int64_t W, n_rows, chunk_rows, next_row;
+};
+
 struct LevelBuffers {
 	rtamd::RayLevel lv{};
 	void* block = nullptr;
@@ -76,6 +86,7 @@ struct Lane {
 	int32_t* counts_host = nullptr;      // pinned, per level: hits, children (levels_cap x 2)
 	// chunk state
 	enum Phase { IDLE, TRACING, FINISHING } phase = IDLE;
+	Job* job = nullptr;                   // the render job the chunk belongs to
 	rtamd::FrameGeometry fg{};
 	int64_t r0 = 0, n0 = 0;
 	int level = 0;                        // the level whose counts are awaited
@@ -99,6 +110,9 @@ struct rt_scene {
 	int64_t out_capacity = 0;
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
 	int direct_levels = 3;
+	int single_lanes = 1;                        // lanes one frame is split over (RTAMD_LANES)
+	int batch_lanes = 2;                         // frames of a batch in flight (RTAMD_BATCH_LANES)
+	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketShadow0;  // measured best on C3
 };
@@ -132,10 +146,10 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	capacity = std::max<int64_t>(capacity, 1024);
 	const int64_t n = capacity;
 	const int64_t nl = std::max(8, s->ds.occl_stride);
-	// 18 double arrays, 4 int32 arrays, inside flags, n x lights shadow verdicts and the
+	// 18 double arrays, 4 int32 arrays, two flag arrays, n x lights shadow verdicts and the
 	// level's counts, each 256-B aligned
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	const int64_t bytes = 18 * align(n * 8) + 4 * align(n * 4) + align(n) + align(n * nl) + 256;
+	const int64_t bytes = 18 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
 	HIP_TRY(hipMalloc(&L.block, bytes));
 	char* p = static_cast<char*>(L.block);
 	auto take = [&](int64_t b) {
@@ -151,6 +165,7 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	L.lv.child_refr = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.child_refl = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.inside = reinterpret_cast<uint8_t*>(take(n));
+	L.lv.hinside = reinterpret_cast<uint8_t*>(take(n));
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
 	HIP_TRY(hipMemset(L.lv.counts, 0, 2 * sizeof(int32_t)));
@@ -227,14 +242,11 @@ void lane_destroy(Lane& ln) {
 	if (ln.stream) (void)hipStreamDestroy(ln.stream);
 }
 
-// The render of one rt_render_device call: chunks of rows handed to lanes, each lane a
-// small state machine advanced by the host as its events complete.
+// The render of one rt_render_device / rt_render_batch_device call: chunks of rows of
+// its jobs handed to lanes, each lane a small state machine advanced by the host as its
+// events complete.
 struct Render {
 	rt_scene* s;
-	int depth, io;
-	double* out_rgb_dev;
-	uint8_t* out_rgb8_dev;
-	int64_t W;
 	rt_counters cnt{};
 	float kernel_ms = 0.f;
 
@@ -242,7 +254,7 @@ struct Render {
 	// with n_dev (the previous level's child counter) an upper bound: the level is queued
 	// behind the previous one before the host knows its size (one level of lookahead).
 	int launch_closest_level(Lane& ln, int L, int64_t n, const int32_t* n_dev) {
-		const int remaining = depth - L;
+		const int remaining = ln.job->depth - L;
 		int rc;
 		// children of this level: at most 2 per ray
 		if (remaining > 0 && (rc = ensure_level_record(s, ln, L + 1, 2 * n))) return rc;
@@ -294,16 +306,18 @@ struct Render {
 		return RT_OK;
 	}
 
-	int start_chunk(Lane& ln, int64_t r0, int64_t rows, const rt_render_params* p) {
+	int start_chunk(Lane& ln, Job& job, int64_t r0, int64_t rows) {
+		const rt_render_params* p = job.p;
+		ln.job = &job;
 		ln.fg = rtamd::FrameGeometry{};
 		ln.fg.width = p->width;
 		ln.fg.height = p->height;
 		ln.fg.row_begin = p->row_begin;
 		ln.fg.row_step = p->row_step;
 		ln.fg.chunk_row0 = static_cast<int32_t>(r0);
-		ln.fg.intersection_only = io;
+		ln.fg.intersection_only = job.io;
 		ln.r0 = r0;
-		ln.n0 = rows * W;
+		ln.n0 = rows * job.W;
 		ln.level = 0;
 		ln.level_n.assign(1, ln.n0);
 		ln.shaded.clear();
@@ -311,7 +325,7 @@ struct Render {
 		ln.phase = Lane::TRACING;
 		int rc = ensure_level_record(s, ln, 0, ln.n0);
 		if (!rc) rc = launch_closest_level(ln, 0, ln.n0, nullptr);
-		if (!rc && depth >= 1) rc = launch_closest_level(ln, 1, 2 * ln.n0, ln.levels[0].lv.counts + 1);
+		if (!rc && job.depth >= 1) rc = launch_closest_level(ln, 1, 2 * ln.n0, ln.levels[0].lv.counts + 1);
 		return rc;
 	}
 
@@ -320,6 +334,8 @@ struct Render {
 	// MathException is reported after the render (the reference aborts; the GPU merely
 	// finishes the chunk).
 	int on_counts(Lane& ln) {
+		const Job& job = *ln.job;
+		const int depth = job.depth;
 		const int L = ln.level;
 		cnt.trace_rays += ln.level_n[L];
 		const int64_t nh = ln.counts_host[2 * L], nn = ln.counts_host[2 * L + 1];
@@ -348,8 +364,10 @@ struct Render {
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
 		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 0; l--)
 			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], ln.levels[l].lv, ln.levels[l + 1].lv, ln.stream));
-		HIP_TRY(rtamd::launch_output(ln.n0, ln.levels[0].lv, out_rgb_dev ? out_rgb_dev + ln.r0 * W * 3 : nullptr,
-		                             out_rgb8_dev ? out_rgb8_dev + ln.r0 * W * 3 : nullptr, io, s->stats, ln.stream));
+		const int64_t W = job.W;
+		HIP_TRY(rtamd::launch_output(ln.n0, ln.levels[0].lv, job.out_rgb_dev ? job.out_rgb_dev + ln.r0 * W * 3 : nullptr,
+		                             job.out_rgb8_dev ? job.out_rgb8_dev + ln.r0 * W * 3 : nullptr, job.io, s->stats,
+		                             ln.stream));
 		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
 		ln.phase = Lane::FINISHING;
 		return RT_OK;
@@ -383,6 +401,22 @@ struct Render {
 int64_t selected_rows(const rt_render_params* p) {
 	if (p->row_step <= 0 || p->row_end <= p->row_begin) return 0;
 	return (p->row_end - p->row_begin + p->row_step - 1) / p->row_step;
+}
+
+constexpr int kMaxLanes = 8;
+
+// the scene has at least n lanes (each: streams, events; level buffers grow on use)
+int ensure_lanes(rt_scene* s, size_t n) {
+	while (s->lanes.size() < n) {
+		std::unique_ptr<Lane> ln(new Lane());
+		const int rc = lane_create(*ln, s->prio_low, s->prio_high);
+		if (rc) {
+			lane_destroy(*ln);
+			return rc;
+		}
+		s->lanes.push_back(std::move(ln));
+	}
+	return RT_OK;
 }
 
 int check_params(const rt_scene* s, const rt_render_params* p) {
@@ -439,24 +473,16 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
 	std::unique_ptr<rt_scene> s(new rt_scene());
 	s->device = device;
-	int n_lanes = 1;  // measured: concurrent chunk pipelines are slower on C3
-	// tuning knobs
+	// tuning knobs; lanes are created on first use
 	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);
 	if (const char* dl = std::getenv("RTAMD_DIRECT_LEVELS")) s->direct_levels = std::max(1, std::atoi(dl));
-	if (const char* nl = std::getenv("RTAMD_LANES")) n_lanes = std::min(8, std::max(1, std::atoi(nl)));
+	if (const char* nl = std::getenv("RTAMD_LANES")) s->single_lanes = std::min(kMaxLanes, std::max(1, std::atoi(nl)));
+	if (const char* bl = std::getenv("RTAMD_BATCH_LANES"))
+		s->batch_lanes = std::min(kMaxLanes, std::max(1, std::atoi(bl)));
 	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
-	int prio_low = 0, prio_high = 0;
-	HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_low, &prio_high));
+	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
-	for (int k = 0; k < n_lanes; k++) {
-		s->lanes.emplace_back(new Lane());
-		int rc = lane_create(*s->lanes.back(), prio_low, prio_high);
-		if (rc) {
-			rt_scene_destroy(s.release());
-			return rc;
-		}
-	}
 	int rc;
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
@@ -524,35 +550,47 @@ int rt_scene_get_info(const rt_scene* s, rt_scene_info* info) {
 	*info = s->info;
 	return RT_OK;
 }
-int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_dev, void* stream_v,
-                     rt_counters* counters) {
-	int rc = check_params(s, p);
+}  // extern "C"
+
+namespace {
+
+// Renders `n` jobs: chunks of at most 4 M pixels are handed to idle lanes, so with several
+// lanes the chunks (of one image, or whole images of a batch) are traced concurrently
+// and one image's latency-bound deep levels overlap another's wide first levels.
+// --intersection-only jobs come one per call (their maximum is a per-image statistic).
+int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters) {
+	const bool batch = jobs.size() > 1;
+	const size_t n_lanes = batch ? std::min<size_t>(jobs.size(), s->batch_lanes) : s->single_lanes;
+	int rc = ensure_lanes(s, n_lanes);
 	if (rc) return rc;
-	HIP_TRY(hipSetDevice(s->device));
-	// The caller's stream is joined first (its prior work, e.g. the allocation of the
-	// output buffers, completes before ours starts); the call returns when all is done.
-	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
-	const int64_t W = p->width;
-	const int64_t n_rows = selected_rows(p);
-	Render R{s, p->intersection_only ? 0 : p->bounce_depth, p->intersection_only != 0, out_rgb_dev, out_rgb8_dev, W};
+	Render R{s};
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
+	// the caller's stream is joined first (its prior work, e.g. the allocation of the
+	// output buffers, completes before ours starts); the call returns when all is done
 	HIP_TRY(hipEventRecord(s->fork_event, caller));
-	for (auto& ln : s->lanes) HIP_TRY(hipStreamWaitEvent(ln->stream, s->fork_event, 0));
-	// chunks: at most 4 M pixels (bounds the level buffers), and enough of them for every
-	// lane to hold `chunks_per_lane` of them
-	const int64_t max_rows = std::max<int64_t>(1, (p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22) / W);
-	const int64_t want = static_cast<int64_t>(s->lanes.size()) * (s->lanes.size() > 1 ? s->chunks_per_lane : 1);
-	const int64_t chunk_rows = std::min(max_rows, std::max<int64_t>(1, (n_rows + want - 1) / want));
-	int64_t next_row = 0;
+	for (size_t k = 0; k < n_lanes; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k]->stream, s->fork_event, 0));
+	for (Job& job : jobs) {
+		// chunks: at most 4 M pixels (bounds the level buffers); one image over several
+		// lanes is split so that every lane holds `chunks_per_lane` of its chunks
+		const rt_render_params* p = job.p;
+		const int64_t max_rows =
+		    std::max<int64_t>(1, (p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22) / job.W);
+		const int64_t want = (!batch && n_lanes > 1) ? static_cast<int64_t>(n_lanes) * s->chunks_per_lane : 1;
+		job.chunk_rows = std::min(max_rows, std::max<int64_t>(1, (job.n_rows + want - 1) / want));
+		job.next_row = 0;
+	}
+	size_t next_job = 0;
 	for (;;) {
 		bool busy = false;
-		for (auto& lp : s->lanes) {
-			Lane& ln = *lp;
+		for (size_t k = 0; k < n_lanes; k++) {
+			Lane& ln = *s->lanes[k];
 			if (ln.phase == Lane::IDLE) {
-				if (next_row >= n_rows) continue;
-				const int64_t rows = std::min(chunk_rows, n_rows - next_row);
-				if ((rc = R.start_chunk(ln, next_row, rows, p))) return rc;
-				next_row += rows;
+				while (next_job < jobs.size() && jobs[next_job].next_row >= jobs[next_job].n_rows) next_job++;
+				if (next_job >= jobs.size()) continue;
+				Job& job = jobs[next_job];
+				const int64_t rows = std::min(job.chunk_rows, job.n_rows - job.next_row);
+				if ((rc = R.start_chunk(ln, job, job.next_row, rows))) return rc;
+				job.next_row += rows;
 				busy = true;
 				continue;
 			}
@@ -575,7 +613,6 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 	const unsigned long long* sum = s->summary_host;
 	if (sum[rtamd::ST_COUNT]) return fail(RT_ERR_MATH, device_error_text(static_cast<int>(sum[rtamd::ST_COUNT])));
 	rt_counters& cnt = R.cnt;
-	const int io = R.io;
 	cnt.shadow_rays = static_cast<int64_t>(sum[rtamd::ST_HITS]) * s->ds.n_nonambient;
 	cnt.reflect_rays = static_cast<int64_t>(sum[rtamd::ST_REFL]);
 	cnt.refract_rays = static_cast<int64_t>(sum[rtamd::ST_REFR]);
@@ -593,19 +630,111 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 		cnt.sphere_tests += cnt.stage_sphere_tests[k];
 	}
 	cnt.trace_launches = cnt.stage_launches[0] + cnt.stage_launches[1] + cnt.stage_launches[2];
-	if (io && sum[rtamd::ST_MAX_BITS]) {
-		double m;
-		const unsigned long long b = sum[rtamd::ST_MAX_BITS];
-		std::memcpy(&m, &b, sizeof(m));
-		cnt.intersection_max = std::max(cnt.intersection_max, m);
-	}
 	cnt.kernel_ms = R.kernel_ms;
-	// full-image --intersection-only: normalise in place (scene.cpp:50-58)
-	if (io && p->row_begin == 0 && p->row_end == p->height && p->row_step == 1 && out_rgb_dev) {
-		HIP_TRY(rtamd::launch_normalize(n_rows * W * 3, out_rgb_dev, cnt.intersection_max, out_rgb8_dev, caller));
-		HIP_TRY(hipStreamSynchronize(caller));
+	if (jobs.size() == 1 && jobs[0].io) {
+		const Job& job = jobs[0];
+		const rt_render_params* p = job.p;
+		if (sum[rtamd::ST_MAX_BITS]) {
+			double m;
+			const unsigned long long b = sum[rtamd::ST_MAX_BITS];
+			std::memcpy(&m, &b, sizeof(m));
+			cnt.intersection_max = std::max(cnt.intersection_max, m);
+		}
+		// full-image --intersection-only: normalise in place (scene.cpp:50-58)
+		if (p->row_begin == 0 && p->row_end == p->height && p->row_step == 1 && job.out_rgb_dev) {
+			HIP_TRY(rtamd::launch_normalize(job.n_rows * job.W * 3, job.out_rgb_dev, cnt.intersection_max,
+			                                job.out_rgb8_dev, caller));
+			HIP_TRY(hipStreamSynchronize(caller));
+		}
 	}
 	if (counters) *counters = cnt;
+	return RT_OK;
+}
+
+Job make_job(const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_dev) {
+	Job j{};
+	j.p = p;
+	j.out_rgb_dev = out_rgb_dev;
+	j.out_rgb8_dev = out_rgb8_dev;
+	j.io = p->intersection_only != 0;
+	j.depth = j.io ? 0 : p->bounce_depth;
+	j.W = p->width;
+	j.n_rows = selected_rows(p);
+	return j;
+}
+
+void add_counters(rt_counters& a, const rt_counters& b) {
+	a.trace_rays += b.trace_rays;
+	a.shadow_rays += b.shadow_rays;
+	a.reflect_rays += b.reflect_rays;
+	a.refract_rays += b.refract_rays;
+	a.pixels += b.pixels;
+	a.intersection_max = std::max(a.intersection_max, b.intersection_max);
+	a.kernel_ms += b.kernel_ms;
+	a.levels = std::max(a.levels, b.levels);
+	a.trace_launches += b.trace_launches;
+	a.node_visits += b.node_visits;
+	a.tri_tests += b.tri_tests;
+	a.candidates += b.candidates;
+	a.sphere_tests += b.sphere_tests;
+	for (int k = 0; k < 3; k++) {
+		a.stage_ms[k] += b.stage_ms[k];
+		a.stage_launches[k] += b.stage_launches[k];
+	}
+	for (int k = 0; k < 2; k++) {
+		a.stage_node_visits[k] += b.stage_node_visits[k];
+		a.stage_tri_tests[k] += b.stage_tri_tests[k];
+		a.stage_candidates[k] += b.stage_candidates[k];
+		a.stage_sphere_tests[k] += b.stage_sphere_tests[k];
+		a.stage_bvh_traversals[k] += b.stage_bvh_traversals[k];
+		a.stage_max_node_visits[k] = std::max(a.stage_max_node_visits[k], b.stage_max_node_visits[k]);
+	}
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_dev, void* stream_v,
+                     rt_counters* counters) {
+	return rt_render_batch_device(s, 1, p, &out_rgb_dev, &out_rgb8_dev, stream_v, counters);
+}
+
+int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params, double* const* out_rgb_dev,
+                           uint8_t* const* out_rgb8_dev, void* stream_v, rt_counters* counters) {
+	if (!s || !params || n < 0) return fail(RT_ERR_ARG, "null scene or params");
+	for (int k = 0; k < n; k++) {
+		const int rc = check_params(s, params + k);
+		if (rc) return rc;
+	}
+	HIP_TRY(hipSetDevice(s->device));
+	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
+	rt_counters total{};
+	total.intersection_max = 2.2250738585072014e-308;
+	std::vector<Job> jobs;
+	auto flush = [&]() -> int {
+		if (jobs.empty()) return RT_OK;
+		rt_counters c{};
+		const int rc = render_jobs(s, jobs, caller, &c);
+		jobs.clear();
+		if (!rc) add_counters(total, c);
+		return rc;
+	};
+	for (int k = 0; k < n; k++) {
+		Job j = make_job(params + k, out_rgb_dev ? out_rgb_dev[k] : nullptr, out_rgb8_dev ? out_rgb8_dev[k] : nullptr);
+		if (j.n_rows <= 0) continue;
+		int rc;
+		if (j.io) {  // alone: its maximum is its own
+			if ((rc = flush())) return rc;
+			jobs.push_back(j);
+			if ((rc = flush())) return rc;
+		} else {
+			jobs.push_back(j);
+		}
+	}
+	const int rc = flush();
+	if (rc) return rc;
+	if (counters) *counters = total;
 	return RT_OK;
 }
 
@@ -651,6 +780,15 @@ int rt_write_png(const char* path, const uint8_t* rgb, int width, int height) {
 	const size_t w = std::fwrite(bytes.data(), 1, bytes.size(), f);
 	std::fclose(f);
 	if (w != bytes.size()) return fail(RT_ERR_IO, "write error");
+	return RT_OK;
+}
+
+// Diagnostic: phase profile of the traversal kernels (RT_PHASE_PROF builds; zeros otherwise),
+// 4 x 8 sums of per-lane shader-clock cycles (trace.h), read and cleared.  Not in rtamd.h.
+int rt_debug_phase_profile(int device, unsigned long long* out32) {
+	HIP_TRY(hipSetDevice(device));
+	HIP_TRY(hipDeviceSynchronize());
+	HIP_TRY(rtamd::read_phase_profile(out32));
 	return RT_OK;
 }
 

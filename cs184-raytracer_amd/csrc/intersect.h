@@ -12,6 +12,9 @@
 // Acceleration (new design, exact): LBVH per mesh, world-space boxes per geometry, and
 // conservative pre-tests that only ever skip work whose outcome is already decided.
 #pragma once
+#ifndef RT_PHASE_PROF
+#define RT_PHASE_PROF 0
+#endif
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include "device_types.h"
@@ -115,7 +118,28 @@ __device__ bool hits_bounding_box(V3 o, V3 d, P mn, P mx) {
 // Per-lane work counters (algorithmic bytes/flops of the roofline)
 struct WorkStats {
 	uint32_t nodes, tris, cands, spheres, bvh_entries;
+#if RT_PHASE_PROF
+	uint32_t ph[kPhaseSlots];  // shader-clock cycles per phase while this lane was active
+#endif
 };
+
+// Phase profile (diagnostic builds, -DRT_PHASE_PROF=1): the wave's shader clock
+// (s_memtime) around code regions, summed per lane.
+enum PhaseSlot : int { PH_TOTAL = 0, PH_NODES, PH_FACES, PH_XFORM, PH_SPHERE, PH_WORLD, PH_SETUP, PH_GATE };
+#if RT_PHASE_PROF
+__device__ __forceinline__ uint32_t prof_t() {
+	__builtin_amdgcn_sched_barrier(0);  // no instruction scheduled across the clock read
+	const uint32_t t = static_cast<uint32_t>(__builtin_amdgcn_s_memtime());
+	__builtin_amdgcn_sched_barrier(0);
+	return t;
+}
+#define PROF_T() prof_t()
+#define PROF_BEGIN(v) const uint32_t v = PROF_T()
+#define PROF_END(ws, k, v) ((ws).ph[k] += PROF_T() - (v))
+#else
+#define PROF_BEGIN(v)
+#define PROF_END(ws, k, v) ((void)0)
+#endif
 
 // A mesh hit (face, barycentric a, b), or a sphere hit (face -1, ray parameter t in a)
 struct FaceHit {
@@ -208,10 +232,16 @@ __device__ __forceinline__ bool slab(P lo, P hi, V3 o, V3 inv, double tlimit, do
 	return tmax >= tmin && tmax >= 0.0 && tmin <= tlimit;
 }
 
-__device__ __forceinline__ V3 safe_inv(V3 d) {
-	return mk(1.0 / (d.x != 0.0 ? d.x : copysign(1e-300, d.x)), 1.0 / (d.y != 0.0 ? d.y : copysign(1e-300, d.y)),
-	          1.0 / (d.z != 0.0 ? d.z : copysign(1e-300, d.z)));
+// 1/x for the slab tests only (conservative, never part of a result): v_rcp_f64 refined by
+// two Newton steps, relative error far below the slabs' 1e-9 widening.  |x| is clamped to
+// >= 1e-300, so the operand and the result are normal numbers.
+__device__ __forceinline__ double slab_rcp(double x) {
+const double a = fabs(x) < 1e-300 ? copysign(1e-300, x) : x;
+double r = __builtin_amdgcn_rcp(a);
+r = fma(r, fma(-a, r, 1.0), r);
+return fma(r, fma(-a, r, 1.0), r);
 }
+__device__ __forceinline__ V3 safe_inv(V3 d) { return mk(slab_rcp(d.x), slab_rcp(d.y), slab_rcp(d.z)); }
 
 __device__ __forceinline__ double prune_limit(double best_dist) { return best_dist * (1.0 + 4e-9); }
 
@@ -224,12 +254,12 @@ __device__ __forceinline__ double prune_limit(double best_dist) { return best_di
 //   dist < any_limit (the caller knows that settles occlusion); nodes beyond
 //   prune_cap are skipped (faces there cannot decide it either).  Otherwise completes
 //   like the closest-hit search restricted to dist <= prune_cap.
+// The search itself, without the reference's bounding-box gate (see mesh_hit).
 template <bool kAnyHit, typename GP>
-__device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
+                         __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
                          double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
                          DeviceCounters* ctr, WorkStats& ws) {
 	settled = false;
-	if (G->gate && !hits_bounding_box(o, d, G->bb_min, G->bb_max)) return false;
 	const double dn = sqrt(d.x * d.x + (d.y * d.y + d.z * d.z));  // Vector3d::norm
 	const V3 nd = -d;
 	MeshBest best;
@@ -237,11 +267,14 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 	best.face = -1;
 	best.id = 0x7fffffff;
 	if (G->bvh_root < 0) {
+		PROF_BEGIN(tf);
 		for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++)
 			if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+				PROF_END(ws, PH_FACES, tf);
 				settled = true;
 				return true;
 			}
+		PROF_END(ws, PH_FACES, tf);
 	} else {
 		// while-while traversal (Aila & Laine 2009): a lane first walks inner nodes until
 		// it holds a leaf, then the lanes holding leaves test their faces together, so
@@ -254,6 +287,7 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 		int sp = 0;
 		auto pop = [&]() { return sp > 0 ? stack[--sp * kBlock] : (int32_t)-1; };
 		while (ref != -1) {
+			PROF_BEGIN(tn);
 			while (ref >= 0) {
 				ws.nodes++;
 				const DBvhNode* N = S.nodes + ref;
@@ -279,14 +313,18 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 					ref = pop();
 				}
 			}
+			PROF_END(ws, PH_NODES, tn);
 			if (ref == -1) break;
 			const int32_t code = -2 - ref;
 			const int32_t f0 = G->face_begin + (code >> 3), f1 = f0 + (code & 7);
+			PROF_BEGIN(tf);
 			for (int32_t f = f0; f < f1; f++)
 				if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+					PROF_END(ws, PH_FACES, tf);
 					settled = true;
 					return true;
 				}
+			PROF_END(ws, PH_FACES, tf);
 			ref = pop();
 		}
 	}
@@ -294,6 +332,22 @@ __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, d
 	if (best.face < 0) return false;
 	fh = FaceHit{best.face, best.a, best.b};
 	return true;
+}
+
+// The reference tests a gated mesh only when hitsBoundingBox passes (geometry.cpp:72); the
+// search has no side effects, so the gate (six divisions) is evaluated only for rays the
+// search reports a hit (or occluder) for: the same outcome for fewer rays.
+template <bool kAnyHit, typename GP>
+__device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
+double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
+DeviceCounters* ctr, WorkStats& ws) {
+if (!mesh_search<kAnyHit>(S, G, o, d, reverse, any_limit, prune_cap, fh, settled, found_dist, stack, ctr, ws))
+return false;
+PROF_BEGIN(tg);
+const bool gate_miss = G->gate && !hits_bounding_box(o, d, G->bb_min, G->bb_max);
+PROF_END(ws, PH_GATE, tg);
+if (gate_miss) settled = false;
+return !gate_miss;
 }
 
 // Sphere::calculateIntNormInObjSpace (geometry.cpp:47-67): the ray parameter t of the
@@ -365,16 +419,23 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
-		if (!slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw)) continue;
+		PROF_BEGIN(tw0);
+		const bool wb = slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw);
+		PROF_END(ws, PH_WORLD, tw0);
+		if (!wb) continue;
 		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
+		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
 		const V3 dd = ray_dir(xf_dir(G->inv, d), ctr);
+		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
 			ws.spheres++;
+			PROF_BEGIN(ts);
 			hit = sphere_hit(G, oo, dd, reverse, h.a);
+		PROF_END(ws, PH_SPHERE, ts);
 		} else {
 			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 		}
@@ -407,18 +468,25 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
-		if (!slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw)) continue;
+		PROF_BEGIN(tw0);
+		const bool wb = slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);
+		PROF_END(ws, PH_WORLD, tw0);
+		if (!wb) continue;
+		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		if (is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
 		const double nrm = sqrt(sq4(draw));  // object-space length of the unit world direction
 		const V3 dd = div3(draw, nrm);
+		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
 		bool hit, settled = false;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
 			ws.spheres++;
+			PROF_BEGIN(ts);
 			hit = sphere_hit(G, oo, dd, reverse, h.a);
+		PROF_END(ws, PH_SPHERE, ts);
 		} else if (inf_light) {
 			hit = mesh_hit<true>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 		} else {
@@ -453,13 +521,16 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 // Callers must reach these functions with all lanes (inactive lanes pass on = false).
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
+// A value every lane holds equally (node and face indices of the packet traversal): read
+// from the first lane, so the compiler keeps it in an SGPR and the node/face records at
+// that index are fetched with scalar loads instead of 64 identical vector loads.
+__device__ __forceinline__ int32_t uniform_i32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 template <bool kAnyHit, typename GP>
 __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, bool on, double any_limit,
                                 double prune_cap, FaceHit& fh, bool& settled, double& found_dist,
                                 int32_t* wstack, WorkStats& ws) {
 	settled = false;
-	if (G->gate) on = on && hits_bounding_box(o, d, G->bb_min, G->bb_max);
 	const double dn = sqrt(d.x * d.x + (d.y * d.y + d.z * d.z));  // Vector3d::norm
 	const V3 nd = -d;
 	MeshBest best;
@@ -469,18 +540,21 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	bool live = on;
 	if (wave_any(live)) {
 		if (G->bvh_root < 0) {
+			PROF_BEGIN(tf);
 			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++)
 				if (live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
 					settled = true;
 					live = false;
 				}
+				PROF_END(ws, PH_FACES, tf);
 		} else {
 			if (live) ws.bvh_entries++;
 			const V3 inv = safe_inv(d);
 			const auto nodes = uniform_ptr(S.nodes);
-			int32_t node = G->bvh_root;
+			int32_t node = uniform_i32(G->bvh_root);
 			int sp = 0;
 			for (;;) {
+				PROF_BEGIN(tn);
 				const auto N = nodes + node;
 				if (live) ws.nodes++;
 				double tn0 = 0, tn1 = 0;
@@ -489,23 +563,26 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				const bool h1 = live && slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
 				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
 				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
-				const int first = (2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0;
+				const int first = uniform_i32((2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0);
 				int32_t next = -1;
+				PROF_END(ws, PH_NODES, tn);
 #pragma unroll
 				for (int k = 0; k < 2; k++) {
 					const int c = first ^ k;
 					bool want = c ? h1 : h0;
 					if (k == 1) want = want && live && (c ? tn1 : tn0) <= fmin(prune_limit(best.dist), prune_cap);
 					if (!wave_any(want)) continue;
-					const int32_t cf = N->first[c], cc = N->count[c];
+					const int32_t cf = uniform_i32(N->first[c]), cc = uniform_i32(N->count[c]);
 					if (cc > 0) {
+						PROF_BEGIN(tf);
 						const int32_t f0 = G->face_begin + cf;
 						for (int32_t f = f0; f < f0 + cc; f++)
 							if (want && live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
 								settled = true;
 								live = false;
 							}
-					} else if (next < 0) {
+							PROF_END(ws, PH_FACES, tf);
+							} else if (next < 0) {
 						next = cf;
 					} else if (sp < kStackDepth) {
 						wstack[sp++] = cf;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
@@ -514,14 +591,22 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				if (!wave_any(live)) break;
 				if (next < 0) {
 					if (sp == 0) break;
-					next = wstack[--sp];
+					next = uniform_i32(wstack[--sp]);
 				}
-				node = next;
+				node = uniform_i32(next);
 			}
 		}
 	}
 	found_dist = best.dist;
-	if (!on || best.face < 0) return false;
+// the reference's gate (geometry.cpp:72), evaluated only for lanes with a result (see mesh_hit)
+bool keep = on && best.face >= 0;
+if (G->gate && wave_any(keep)) {
+PROF_BEGIN(tg);
+if (keep) keep = hits_bounding_box(o, d, G->bb_min, G->bb_max);
+PROF_END(ws, PH_GATE, tg);
+if (!keep) settled = false;
+}
+	if (!keep) return false;
 	fh = FaceHit{best.face, best.a, best.b};
 	return true;
 }
@@ -536,18 +621,24 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
+		PROF_BEGIN(tw0);
 		const bool cand = on && slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw);
+		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
+		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
 		const V3 dd = div3(draw, sqrt(sq4(draw)));
+		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
 			if (cand) ws.spheres++;
+			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
+		PROF_END(ws, PH_SPHERE, ts);
 		} else {
 			hit = mesh_hit_packet<false>(S, G, oo, dd, reverse, cand, INFINITY, INFINITY, h, settled, fd, wstack, ws);
 		}
@@ -577,19 +668,25 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
+		PROF_BEGIN(tw0);
 		const bool cand = on && !occ && slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);
+		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
+		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
 		const double nrm = sqrt(sq4(draw));
 		const V3 dd = div3(draw, nrm);
+		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
 		bool hit, settled = false;
 		double fd = INFINITY;
 		if (G->kind == DGEOM_SPHERE) {
 			if (cand) ws.spheres++;
+			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
+		PROF_END(ws, PH_SPHERE, ts);
 		} else {
 			const double tl = inf_light ? INFINITY : dist_light * nrm;
 			const double cap = inf_light ? INFINITY : tl * (1.0 + 1e-7) + 1e-300;

@@ -31,10 +31,12 @@ struct RayLevel {
 	uint8_t* inside;
 	// closest hit (k_closest -> k_shadow, k_shade)
 	int32_t* hgeom;              // hit geometry, -1 = miss
+	// hit records, compacted: entry h (0 <= h < counts[0]) is the h-th hit found, ray hit_list[h]
 	double *hpx, *hpy, *hpz;     // world hit point
 	double *hnx, *hny, *hnz;     // shading normal (flipped if inside, normalised)
-	int32_t* hit_list;           // indices of rays that hit (order of discovery)
-	uint8_t* occl;               // [ray][non-ambient light] shadow verdicts
+	uint8_t* hinside;            // the ray's inside flag
+	int32_t* hit_list;           // ray index of each hit (order of discovery)
+	uint8_t* occl;               // [hit][non-ambient light] shadow verdicts
 	// node out
 	double *cr, *cg, *cb;        // local colour, overwritten with the final colour by reduce
 	double *kr, *kg, *kb;        // reflective weight (after TIR), valid when child_refl >= 0
@@ -76,8 +78,12 @@ constexpr int kStatStride = 16;  // u64 per shard (128 B)
 // `next` (count cur.counts[1]).  The shading of level L (shadow rays, then Phong terms)
 // depends only on k_closest(L), so it runs on a second stream while k_closest(L+1)
 // traces the children: the latency-bound deep levels overlap with shading work.
-// packet_mask selects wave-packet traversal per kernel and level class
-enum : int { kPacketClosest0 = 1, kPacketClosestN = 2, kPacketShadow0 = 4, kPacketShadowN = 8 };
+// packet_mask selects wave-packet traversal per kernel and level class (N: every level
+// >= 1; 1: level 1 only)
+enum : int {
+	kPacketClosest0 = 1, kPacketClosestN = 2, kPacketShadow0 = 4, kPacketShadowN = 8,
+	kPacketClosest1 = 16, kPacketShadow1 = 32
+};
 // n: the level's ray count (level 0), or with n_dev (the previous level's child counter,
 // read on the device) an upper bound used only to size the grid.  levels_dev: the device
 // copy of the RayLevel records (level and level + 1 must be current).
@@ -108,6 +114,11 @@ hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8
 hipError_t launch_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary,
                                hipStream_t stream);
 hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uint8_t* out_rgb8, hipStream_t stream);
+// Phase profile (builds with -DRT_PHASE_PROF=1 only, else zeros): per (stage, packet) pair
+// (stage 0 k_closest, 1 k_shadow) 8 sums of per-lane shader-clock cycles (intersect.h
+// PhaseSlot); copied and cleared.
+constexpr int kPhaseSlots = 8;
+hipError_t read_phase_profile(unsigned long long* out /* 4 * kPhaseSlots */);
 hipError_t launch_selftest_math(int op, const double* x, const double* y, double* out, int64_t n, hipStream_t stream);
 
 }  // namespace rtamd

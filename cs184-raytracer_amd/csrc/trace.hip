@@ -22,6 +22,16 @@ namespace {
 
 using namespace dev;
 
+// q = n / d for 0 <= n < 2^52, 0 < d (both exact in binary64): the quotient of the
+// doubles, corrected by one step (the rounded quotient is within 1 of the exact one).
+// A 64-bit integer division is a long emulated sequence on the GPU.
+__device__ __forceinline__ int64_t div_small(int64_t n, int64_t d) {
+	int64_t q = static_cast<int64_t>(static_cast<double>(n) / static_cast<double>(d));
+	const int64_t r = n - q * d;
+	q += (r < 0) ? -1 : (r >= d ? 1 : 0);
+	return q;
+}
+
 constexpr int kShadeBlock = 512;
 
 // Occupancy targets of the traversal kernels (waves per SIMD); 0 = compiler's choice.
@@ -41,6 +51,10 @@ constexpr int kShadeBlock = 512;
 #define RT_CLOSEST_ATTR __attribute__((amdgpu_waves_per_eu(RT_CLOSEST_WAVES)))
 #else
 #define RT_CLOSEST_ATTR
+#endif
+// the wave-packet variants keep node and face records in SGPRs and need fewer VGPRs
+#ifndef RT_PACKET_WAVES
+#define RT_PACKET_WAVES RT_TRAVERSAL_WAVES
 #endif  // 8 waves: one child-allocation atomic per 512 rays
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
@@ -61,9 +75,10 @@ template <typename LV>
 __device__ __forceinline__ void level_ray(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t i,
                                           const LV& cur, V3& o, V3& d, bool& inside, DeviceCounters* ctr) {
 	if (level == 0) {
-		const int64_t row_ord = fg.chunk_row0 + i / fg.width;
+		const int64_t q = div_small(i, fg.width);
+		const int64_t row_ord = fg.chunk_row0 + q;
 		const int r = fg.row_begin + (int)row_ord * fg.row_step;
-		const int c = (int)(i % fg.width);
+		const int c = (int)(i - q * fg.width);
 		primary_ray(S.cam, r, c, fg.width, fg.height, o, d, ctr);
 		inside = false;
 	} else {
@@ -76,10 +91,11 @@ __device__ __forceinline__ void level_ray(const DeviceScene& S, const FrameGeome
 // Level-0 thread -> pixel mapping in 8x8 tiles (one wave = one tile), so primary rays,
 // their shadow rays and their children are spatially coherent.  Returns -1 outside.
 __device__ __forceinline__ int64_t tile_pixel(const FrameGeometry& fg, int64_t n, int64_t t) {
-	const int64_t W = fg.width, R = n / fg.width;
+	const int64_t W = fg.width, R = div_small(n, fg.width);
 	const int64_t tiles_x = (W + 7) / 8;
 	const int64_t tile = t >> 6, l = t & 63;
-	const int64_t px = (tile % tiles_x) * 8 + (l & 7), py = (tile / tiles_x) * 8 + (l >> 3);
+	const int64_t ty = div_small(tile, tiles_x);
+	const int64_t px = (tile - ty * tiles_x) * 8 + (l & 7), py = ty * 8 + (l >> 3);
 	return (px < W && py < R) ? py * W + px : -1;
 }
 __host__ __device__ __forceinline__ int64_t tile_threads(int64_t n, int64_t width) {
@@ -110,7 +126,19 @@ __device__ __forceinline__ unsigned long long* shard(unsigned long long* stats) 
 	return stats + (blockIdx.x % kStatShards) * kStatStride;
 }
 
-__device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long long* stats, int stage) {
+#if RT_PHASE_PROF
+__device__ unsigned long long g_phase[4 * kPhaseSlots];  // [stage * 2 + packet][slot]
+#endif
+
+__device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long long* stats, int stage, int packet = 0) {
+	#if RT_PHASE_PROF
+	#pragma unroll
+	for (int k = 0; k < kPhaseSlots; k++) {
+	unsigned long long v = ws.ph[k];
+	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+	if (__lane_id() == 0 && v) atomicAdd(&g_phase[(stage * 2 + packet) * kPhaseSlots + k], v);
+	}
+	#endif
 	unsigned long long w[5] = {ws.nodes, ws.tris, ws.cands, ws.spheres, ws.bvh_entries};
 	unsigned long long wmax = ws.nodes;
 #pragma unroll
@@ -178,19 +206,23 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
                                              AppendLds& append_lds, int32_t* stack) {
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
-	WorkStats ws{0, 0, 0, 0, 0};
+	WorkStats ws{};
+	PROF_BEGIN(t_total);
 	bool hit = false;
 	int gi = -1;
 	double dist = 0;
 	V3 P = mk(0, 0, 0), N = mk(0, 0, 0), Nobj = mk(0, 0, 0);
 	bool inside = false;
 	V3 o = mk(0, 0, 0), d = mk(0, 0, 1);
+	PROF_BEGIN(t_setup);
 	if (active) level_ray(S, fg, level, i, cur, o, d, inside, ctr);
+	PROF_END(ws, PH_SETUP, t_setup);
 	if (kPacket)
 		hit = closest_hit_packet(S, o, d, inside, active, dist, gi, P, Nobj, stack, ctr, ws);
 	else if (active)
 		hit = closest_hit(S, o, d, inside, dist, gi, P, Nobj, stack, ctr, ws);
-	flush_stats(ws, stats, 0);
+	if (active) PROF_END(ws, PH_TOTAL, t_total);
+	flush_stats(ws, stats, 0, kPacket);
 	if (hit) {
 		// Geometry::calculateIntersectionNormal tail (geometry.cpp:40-43) + scene.cpp:72-75
 		N = xf_normal(S.geoms[gi].inv, Nobj);
@@ -276,13 +308,16 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 		cur.cr[i] = cur.cg[i] = cur.cb[i] = 0.0;
 		return;
 	}
-	cur.hpx[i] = P.x;
-	cur.hpy[i] = P.y;
-	cur.hpz[i] = P.z;
-	cur.hnx[i] = N.x;
-	cur.hny[i] = N.y;
-	cur.hnz[i] = N.z;
-	cur.hit_list[slot.a] = (int32_t)i;
+	// the hit record, compacted at the hit's slot: k_shadow reads it without indirection
+	const int64_t h = slot.a;
+	cur.hpx[h] = P.x;
+	cur.hpy[h] = P.y;
+	cur.hpz[h] = P.z;
+	cur.hnx[h] = N.x;
+	cur.hny[h] = N.y;
+	cur.hnz[h] = N.z;
+	cur.hinside[h] = inside;
+	cur.hit_list[h] = (int32_t)i;
 }
 
 // Level 0: one thread per pixel (n_dev null, exact grid).  Deeper levels are launched
@@ -290,7 +325,8 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 // child counter (n_dev) and a fixed grid strides over it, so each level is queued behind
 // the previous one without a host round trip.
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock) RT_CLOSEST_ATTR k_closest(DeviceScene S, FrameGeometry fg, int level,
+__global__ void __launch_bounds__(kBlock)
+    __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
                                                                       int64_t n_host, const int32_t* n_dev,
                                                                       int remaining, const RayLevel* levels,
                                                                       DeviceCounters* ctr,
@@ -327,7 +363,8 @@ __device__ __forceinline__ BatchItem batch_item(const ShadeBatch& B, const int64
 // Shadow rays: item t of a level -> (light j = t / nh, hit h = t % nh), light-major so a
 // wave traces rays towards one light from neighbouring hits (scene.cpp:87-93).
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene S, ShadeBatch B,
+__global__ void __launch_bounds__(kBlock)
+    __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
@@ -338,33 +375,36 @@ __global__ void __launch_bounds__(kBlock) RT_TRAVERSAL_ATTR k_shadow(DeviceScene
 	const int64_t t = it.local, nh = it.nh;
 	const auto& cur = *uniform_ptr(levels + level);
 	const int nl = S.n_nonambient;
-	WorkStats ws{0, 0, 0, 0, 0};
+	WorkStats ws{};
+	PROF_BEGIN(t_total);
 	const bool on = t < nh * nl;
-	int32_t i = 0;
+	int64_t h = 0;
 	int j = 0;
 	V3 P = mk(0, 0, 0), Ld = mk(0, 0, 1);
 	bool rev = false;
 	double dL = 0;
 	if (on) {
-		j = (int)(t / nh);
-		i = cur.hit_list[t % nh];
+		j = (int)div_small(t, nh);
+		h = t - j * nh;
 		const DLight& L = S.lights[S.shadow_light[j]];
-		P = mk(cur.hpx[i], cur.hpy[i], cur.hpz[i]);
-		const V3 N = mk(cur.hnx[i], cur.hny[i], cur.hnz[i]);
-		const bool inside = level ? cur.inside[i] : false;
+		P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
+		const V3 N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
+		const bool inside = cur.hinside[h];
 		const bool point = L.kind == DLIGHT_POINT;
 		const V3 lv = load3(L.vec);
 		Ld = ray_dir(point ? lv - P : -lv, ctr);  // Light::calculateRayToLight
 		rev = (dot4z(N, Ld) < 0) ^ inside;
 		dL = point ? sqrt(sq4(lv - P)) : INFINITY;
 	}
+	if (on) PROF_END(ws, PH_SETUP, t_total);
 	bool occ = false;
 	if (kPacket)
 		occ = occluded_packet(S, P, Ld, rev, dL, on, stack, ctr, ws);
 	else if (on)
 		occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
-	if (on) cur.occl[(int64_t)i * S.occl_stride + j] = occ;
-	flush_stats(ws, stats, 1);
+	if (on) cur.occl[h * S.occl_stride + j] = occ;
+	if (on) PROF_END(ws, PH_TOTAL, t_total);
+	flush_stats(ws, stats, 1, kPacket);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -381,16 +421,17 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	if (it.local >= it.nh) return;
 	const int level = it.level;
 	const auto& cur = *uniform_ptr(levels + level);
-	const int64_t i = cur.hit_list[it.local];
+	const int64_t hs = it.local;  // the hit's slot (hit records, verdicts)
+	const int64_t i = cur.hit_list[hs];
 	const int gi = cur.hgeom[i];
 	double col[3] = {0.0, 0.0, 0.0};
 	V3 o, d;
 	bool inside;
 	level_ray(S, fg, level, i, cur, o, d, inside, ctr);
-	const V3 P = mk(cur.hpx[i], cur.hpy[i], cur.hpz[i]);
-	const V3 N = mk(cur.hnx[i], cur.hny[i], cur.hnz[i]);
+	const V3 P = mk(cur.hpx[hs], cur.hpy[hs], cur.hpz[hs]);
+	const V3 N = mk(cur.hnx[hs], cur.hny[hs], cur.hnz[hs]);
 	const DMaterial& M = S.mats[S.geoms[gi].mat];
-	const uint64_t* occ_words = reinterpret_cast<const uint64_t*>(cur.occl + i * S.occl_stride);
+	const uint64_t* occ_words = reinterpret_cast<const uint64_t*>(cur.occl + hs * S.occl_stride);
 	uint64_t occ_word = 0;
 	int j = 0;
 	for (int li = 0; li < S.n_lights; li++) {
@@ -543,7 +584,7 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
                           int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
                           unsigned long long* stats, hipStream_t stream, int packet_mask) {
 	if (n <= 0) return hipSuccess;
-	const bool packet = packet_mask & (level == 0 ? kPacketClosest0 : kPacketClosestN);
+	const bool packet = packet_mask & (level == 0 ? kPacketClosest0 : level == 1 ? kPacketClosestN | kPacketClosest1 : kPacketClosestN);
 	const int64_t threads = (level == 0 && packet) ? tile_threads(n, fg.width) : n;
 	// with a device-side count, n is an upper bound: a grid of at most kStrideBlocks
 	const unsigned grid = n_dev ? (unsigned)std::min<int64_t>(grid_for(threads, kBlock), kStrideBlocks)
@@ -561,7 +602,8 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
                          unsigned long long* stats, hipStream_t stream, int packet_mask) {
 	const int64_t items = b.shadow_begin[b.n];
 	if (items <= 0 || s.n_nonambient <= 0) return hipSuccess;
-	if (packet_mask & (b.level[0] == 0 ? kPacketShadow0 : kPacketShadowN))
+	const int lv = b.level[0];
+	if (packet_mask & (lv == 0 ? kPacketShadow0 : (lv == 1 && b.n == 1) ? kPacketShadowN | kPacketShadow1 : kPacketShadowN))
 		hipLaunchKernelGGL(k_shadow<true>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, b, levels_dev, ctr,
 		                   stats);
 	else
@@ -603,6 +645,18 @@ hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uin
 	const double rcp = 1.0 / max_value;  // Color3d /= scalar: multiply by the reciprocal
 	hipLaunchKernelGGL(k_normalize, dim3(grid_for(n_values, 256)), dim3(256), 0, stream, n_values, rgb, rcp, out_rgb8);
 	return hipGetLastError();
+}
+
+hipError_t read_phase_profile(unsigned long long* out) {
+#if RT_PHASE_PROF
+	hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase));
+	if (e != hipSuccess) return e;
+	static const unsigned long long zero[4 * kPhaseSlots] = {};
+	return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), zero, sizeof(zero));
+#else
+	for (int k = 0; k < 4 * kPhaseSlots; k++) out[k] = 0;
+	return hipSuccess;
+#endif
 }
 
 hipError_t launch_selftest_math(int op, const double* x, const double* y, double* out, int64_t n, hipStream_t stream) {

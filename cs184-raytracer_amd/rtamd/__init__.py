@@ -17,12 +17,13 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional
+from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librtamd.so")
+# RTAMD_LIB: an alternative build of the same library (e.g. the phase-profile build, make prof)
+LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(_HERE, "librtamd.so")
 
 RT_OK, RT_ERR_PARSE, RT_ERR_MATH, RT_ERR_ARG, RT_ERR_DEVICE, RT_ERR_IO = 0, -1, -2, -3, -4, -5
 
@@ -107,6 +108,8 @@ def lib() -> ctypes.CDLL:
         "rt_scene_get_info": (i32, [vp, ctypes.POINTER(rt_scene_info)]),
         "rt_render": (i32, [vp, ctypes.POINTER(rt_render_params), vp, PROGRESS_FN, vp, ctypes.POINTER(rt_counters)]),
         "rt_render_device": (i32, [vp, ctypes.POINTER(rt_render_params), vp, vp, vp, ctypes.POINTER(rt_counters)]),
+        "rt_render_batch_device": (i32, [vp, i32, ctypes.POINTER(rt_render_params), ctypes.POINTER(vp),
+                                         ctypes.POINTER(vp), vp, ctypes.POINTER(rt_counters)]),
         "rt_normalize_device": (i32, [vp, vp, i64, dbl, vp, vp]),
         "rt_to_rgb8": (None, [vp, i64, vp]),
         "rt_write_png": (i32, [cp, vp, i32, i32]),
@@ -273,6 +276,19 @@ class Scene:
         cnt = rt_counters()
         _raise(lib().rt_render_device(self.handle, ctypes.byref(params), out_rgb_ptr or None, out_rgb8_ptr or None,
                                       stream_ptr or None, ctypes.byref(cnt)))
+        self.last_stats = _stats(cnt)
+        return self.last_stats
+
+    def render_batch_device(self, params: Sequence[rt_render_params], out_rgb_ptrs: Sequence[int] = (),
+                            out_rgb8_ptrs: Sequence[int] = (), stream_ptr: int = 0) -> RenderStats:
+        """rt_render_batch_device: len(params) renders, images pipelined over the scene's lanes;
+        missing/0 pointers are NULL.  Stats are sums over the batch."""
+        n = len(params)
+        prm = (rt_render_params * max(n, 1))(*params)
+        ptrs = lambda xs: (ctypes.c_void_p * max(n, 1))(*[(xs[k] if k < len(xs) else 0) or None for k in range(n)])
+        cnt = rt_counters()
+        _raise(lib().rt_render_batch_device(self.handle, n, prm, ptrs(out_rgb_ptrs), ptrs(out_rgb8_ptrs),
+                                            stream_ptr or None, ctypes.byref(cnt)))
         self.last_stats = _stats(cnt)
         return self.last_stats
 

@@ -101,7 +101,7 @@ typedef struct rt_counters {
 	double  stage_ms[3];
 	int32_t stage_launches[3];
 	int64_t stage_node_visits[2], stage_tri_tests[2], stage_candidates[2], stage_sphere_tests[2];
-	int64_t stage_bvh_traversals[2];   /* mesh LBVH traversals started (after the mesh gate) */
+	int64_t stage_bvh_traversals[2];   /* mesh LBVH traversals started (the mesh gate is tested after) */
 	int64_t stage_max_node_visits[2];  /* most LBVH nodes one ray visited (all meshes)       */
 } rt_counters;
 
@@ -119,6 +119,16 @@ int rt_render(rt_scene* s, const rt_render_params* p, double* out_rgb,
  * the work on it is complete. */
 int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev,
                      uint8_t* out_rgb8_dev, void* stream, rt_counters* counters);
+
+/* A batch of n renders of the scene (params[k] -> out_rgb_dev[k], out_rgb8_dev[k]; either
+ * array, or any entry, may be NULL), each equal to its own rt_render_device call.  Up to
+ * RTAMD_BATCH_LANES (default 2) images are traced concurrently, so one image's
+ * latency-bound deep reflection levels overlap the next image's wide first levels
+ * (frame pipelining for throughput; the reference renders one image per renderScene).
+ * intersection_only entries are rendered one at a time.  counters: sums over the batch. */
+int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params,
+                           double* const* out_rgb_dev, uint8_t* const* out_rgb8_dev,
+                           void* stream, rt_counters* counters);
 
 /* In-place scale of a device f64 image by 1/max (the --intersection-only tail of
  * scene.cpp:56, Color3d /= scalar == multiply by the reciprocal) + optional rgb8. */
