@@ -114,7 +114,10 @@ struct rt_scene {
 	int batch_lanes = 2;                         // frames of a batch in flight (RTAMD_BATCH_LANES)
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
-	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketShadow0;  // measured best on C3
+	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
+	// measured best on C3: packets for the camera rays, their first bounce and the
+	// camera rays' shadow rays
+	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketClosest1 | rtamd::kPacketShadow0;
 };
 
 namespace {
@@ -287,11 +290,12 @@ struct Render {
 			b.nh[k] = lv[k].second;
 			b.shadow_begin[k] = so;
 			b.shade_begin[k] = ho;
-			so += wave_up(lv[k].second * nl);
+			so += nl * wave_up(lv[k].second);  // every light's items start on a wave boundary
 			ho += wave_up(lv[k].second);
 		}
 		b.shadow_begin[b.n] = so;
 		b.shade_begin[b.n] = ho;
+		if (s->serial) q = ln.stream;
 		const int first = lv.front().first, last = lv.back().first;
 		const auto& ev = ln.level_events[first];
 		HIP_TRY(hipStreamWaitEvent(q, ln.level_events[last][1], 0));
@@ -480,6 +484,7 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	if (const char* bl = std::getenv("RTAMD_BATCH_LANES"))
 		s->batch_lanes = std::min(kMaxLanes, std::max(1, std::atoi(bl)));
 	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
+	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));

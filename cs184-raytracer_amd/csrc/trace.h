@@ -98,7 +98,7 @@ struct ShadeBatch {
 	int32_t n;                           // levels in the batch
 	int32_t level[kMaxBatch];
 	int64_t nh[kMaxBatch];               // hits of each level (cur.counts[0])
-	int64_t shadow_begin[kMaxBatch + 1]; // k_shadow item ranges: nh * n_nonambient each
+	int64_t shadow_begin[kMaxBatch + 1]; // k_shadow item ranges: n_nonambient x nh rounded up to 64 each
 	int64_t shade_begin[kMaxBatch + 1];  // k_shade item ranges: nh each
 };
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,

@@ -346,22 +346,23 @@ __global__ void __launch_bounds__(kBlock)
 		closest_item<kPacket>(S, fg, level, n, remaining, cur, next, ctr, stats, base + threadIdx.x, append_lds, stack);
 }
 
-// Level of item t of a batch (wave-uniform: every level's items start on a wave boundary)
+// Level of item t of a batch (wave-uniform: every level's items start on a wave boundary,
+// so the level is found from the wave's first item, in scalar registers)
 struct BatchItem {
 	int32_t level;
 	int64_t local, nh;
 };
 __device__ __forceinline__ BatchItem batch_item(const ShadeBatch& B, const int64_t* begin, int64_t t) {
-	BatchItem r{B.level[0], t - begin[0], B.nh[0]};
-#pragma unroll
-	for (int k = 1; k < kMaxBatch; k++)
-		if (k < B.n && t >= begin[k]) r = BatchItem{B.level[k], t - begin[k], B.nh[k]};
-	r.level = __builtin_amdgcn_readfirstlane(r.level);
-	return r;
+const int64_t t0 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(t & ~int64_t(63))) |
+(static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int32_t>(t >> 32))) << 32);
+int k = 0;
+while (k + 1 < B.n && t0 >= begin[k + 1]) k++;
+return BatchItem{B.level[k], t - begin[k], B.nh[k]};
 }
 
-// Shadow rays: item t of a level -> (light j = t / nh, hit h = t % nh), light-major so a
-// wave traces rays towards one light from neighbouring hits (scene.cpp:87-93).
+// Shadow rays: item t of a level -> (light j, hit h) with t = j * nh64 + h, nh64 = nh rounded
+// up to a multiple of 64: light-major, and every wave traces rays towards ONE light (its
+// record is read with scalar loads) from neighbouring hits (scene.cpp:87-93).
 template <bool kPacket>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
@@ -377,16 +378,19 @@ __global__ void __launch_bounds__(kBlock)
 	const int nl = S.n_nonambient;
 	WorkStats ws{};
 	PROF_BEGIN(t_total);
-	const bool on = t < nh * nl;
-	int64_t h = 0;
+	const int64_t nh64 = (nh + 63) & ~int64_t(63);
+	// the wave's light: j = t0 / nh64 for its first item t0 (a few scalar steps: nl <= 64)
+	const int64_t t0 = t - (threadIdx.x & 63);
 	int j = 0;
+	while (j + 1 < nl && t0 >= (j + 1) * nh64) j++;
+	j = __builtin_amdgcn_readfirstlane(j);
+	const int64_t h = t - j * nh64;
+	const bool on = h < nh;
 	V3 P = mk(0, 0, 0), Ld = mk(0, 0, 1);
 	bool rev = false;
 	double dL = 0;
 	if (on) {
-		j = (int)div_small(t, nh);
-		h = t - j * nh;
-		const DLight& L = S.lights[S.shadow_light[j]];
+	const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
 		P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
 		const V3 N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
 		const bool inside = cur.hinside[h];
