@@ -458,54 +458,65 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 // t well inside the light distance occludes (the closest face is nearer still), and no
 // face up to slightly beyond it means no occlusion.  Only a closest face within a
 // relative 1e-7 of the light distance falls back to the reference's full comparison.
+// geom_occludes: geometry G (its world box already passed) occludes the shadow ray.
+template <typename GP>
+__device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double dist_light,
+                              int32_t* stack, DeviceCounters* ctr, WorkStats& ws) {
+	const bool inf_light = dist_light == INFINITY;
+	PROF_BEGIN(tx);
+	const V3 oo = xf_point(G->inv, o);
+	const V3 draw = xf_dir(G->inv, d);
+	if (is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
+	const double nrm = sqrt(sq4(draw));  // object-space length of the unit world direction
+	const V3 dd = div3(draw, nrm);
+	PROF_END(ws, PH_XFORM, tx);
+	FaceHit h{-1, 0, 0};
+	bool hit, settled = false;
+	double fd;
+	if (G->kind == DGEOM_SPHERE) {
+		ws.spheres++;
+		PROF_BEGIN(ts);
+		hit = sphere_hit(G, oo, dd, reverse, h.a);
+		PROF_END(ws, PH_SPHERE, ts);
+	} else if (inf_light) {
+		hit = mesh_hit<true>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
+	} else {
+		// world distance of object-space dist t is ~ t / nrm
+		const double tl = dist_light * nrm;
+		const double cap = tl * (1.0 + 1e-7) + 1e-300;
+		hit = mesh_hit<true>(S, G, oo, dd, reverse, tl * (1.0 - 1e-7), cap, h, settled, fd, stack, ctr, ws);
+		// No face up to `cap` was missed by the capped search, so a closest face beyond
+		// it lies beyond the light.  A closest face inside the 1e-7 band is decided
+		// exactly from the reference's own face choice (full closest-face search).
+		if (hit && !settled) {
+			if (fd > cap) return false;
+			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
+		}
+	}
+	if (!hit) return false;
+	if (inf_light || settled) return true;
+	const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
+	return sqrt(sq4(Pw - o)) <= dist_light;
+}
+
+__device__ __forceinline__ double shadow_slab_limit(double dist_light) {
+	return dist_light == INFINITY ? INFINITY : dist_light * (1.0 + 1e-6);
+}
+
+// The `any` over the geometries, cheap ones first (DeviceScene::shadow_order).
 __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, int32_t* stack,
                          DeviceCounters* ctr, WorkStats& ws) {
 	const V3 winv = safe_inv(d);
-	const bool inf_light = dist_light == INFINITY;
+	const double lim = shadow_slab_limit(dist_light);
 	check_may_raise(S, d, true, ctr);
-	// `any` over the geometries: cheap ones first (DeviceScene::shadow_order)
 	for (int k = 0; k < S.n_geoms; k++) {
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		double tw;
 		PROF_BEGIN(tw0);
-		const bool wb = slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);
+		const bool wb = slab(G->wlo, G->whi, o, winv, lim, tw);
 		PROF_END(ws, PH_WORLD, tw0);
-		if (!wb) continue;
-		PROF_BEGIN(tx);
-		const V3 oo = xf_point(G->inv, o);
-		const V3 draw = xf_dir(G->inv, d);
-		if (is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
-		const double nrm = sqrt(sq4(draw));  // object-space length of the unit world direction
-		const V3 dd = div3(draw, nrm);
-		PROF_END(ws, PH_XFORM, tx);
-		FaceHit h{-1, 0, 0};
-		bool hit, settled = false;
-		double fd;
-		if (G->kind == DGEOM_SPHERE) {
-			ws.spheres++;
-			PROF_BEGIN(ts);
-			hit = sphere_hit(G, oo, dd, reverse, h.a);
-		PROF_END(ws, PH_SPHERE, ts);
-		} else if (inf_light) {
-			hit = mesh_hit<true>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
-		} else {
-			// world distance of object-space dist t is ~ t / nrm
-			const double tl = dist_light * nrm;
-			const double cap = tl * (1.0 + 1e-7) + 1e-300;
-			hit = mesh_hit<true>(S, G, oo, dd, reverse, tl * (1.0 - 1e-7), cap, h, settled, fd, stack, ctr, ws);
-			// No face up to `cap` was missed by the capped search, so a closest face beyond
-			// it lies beyond the light.  A closest face inside the 1e-7 band is decided
-			// exactly from the reference's own face choice (full closest-face search).
-			if (hit && !settled) {
-				if (fd > cap) continue;
-				hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
-			}
-		}
-		if (!hit) continue;
-		if (inf_light || settled) return true;
-		const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
-		if (sqrt(sq4(Pw - o)) <= dist_light) return true;
+		if (wb && geom_occludes(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
 	}
 	return false;
 }

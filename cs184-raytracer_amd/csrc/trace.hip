@@ -34,28 +34,19 @@ __device__ __forceinline__ int64_t div_small(int64_t n, int64_t d) {
 
 constexpr int kShadeBlock = 512;
 
-// Occupancy targets of the traversal kernels (waves per SIMD); 0 = compiler's choice.
-// 4 (<= 128 VGPRs, a few spills) measured 3 % faster than the compiler's 3 on C3.
+// Occupancy targets of the traversal kernels (waves per SIMD, >= 1).  4 (<= 128 VGPRs, a
+// few spills) measured 3 % faster than the compiler's 3 on C3; the wave-packet variants
+// (node and face records in SGPRs) measured best at 4 as well: more waves of them starve
+// the closest-hit chain.
 #ifndef RT_TRAVERSAL_WAVES
 #define RT_TRAVERSAL_WAVES 4
 #endif
 #ifndef RT_CLOSEST_WAVES
 #define RT_CLOSEST_WAVES RT_TRAVERSAL_WAVES
 #endif
-#if RT_TRAVERSAL_WAVES > 0
-#define RT_TRAVERSAL_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRAVERSAL_WAVES)))
-#else
-#define RT_TRAVERSAL_ATTR
-#endif
-#if RT_CLOSEST_WAVES > 0
-#define RT_CLOSEST_ATTR __attribute__((amdgpu_waves_per_eu(RT_CLOSEST_WAVES)))
-#else
-#define RT_CLOSEST_ATTR
-#endif
-// the wave-packet variants keep node and face records in SGPRs and need fewer VGPRs
 #ifndef RT_PACKET_WAVES
 #define RT_PACKET_WAVES RT_TRAVERSAL_WAVES
-#endif  // 8 waves: one child-allocation atomic per 512 rays
+#endif
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
 __device__ __forceinline__ void primary_ray(const DCamera& cam, int r, int c, int W, int H, V3& o, V3& d,
@@ -131,14 +122,14 @@ __device__ unsigned long long g_phase[4 * kPhaseSlots];  // [stage * 2 + packet]
 #endif
 
 __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long long* stats, int stage, int packet = 0) {
-	#if RT_PHASE_PROF
-	#pragma unroll
+#if RT_PHASE_PROF
+#pragma unroll
 	for (int k = 0; k < kPhaseSlots; k++) {
-	unsigned long long v = ws.ph[k];
-	for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-	if (__lane_id() == 0 && v) atomicAdd(&g_phase[(stage * 2 + packet) * kPhaseSlots + k], v);
+		unsigned long long v = ws.ph[k];
+		for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+		if (__lane_id() == 0 && v) atomicAdd(&g_phase[(stage * 2 + packet) * kPhaseSlots + k], v);
 	}
-	#endif
+#endif
 	unsigned long long w[5] = {ws.nodes, ws.tris, ws.cands, ws.spheres, ws.bvh_entries};
 	unsigned long long wmax = ws.nodes;
 #pragma unroll
