@@ -115,6 +115,7 @@ struct rt_scene {
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
+	int shadow_all_lights = 0;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// measured best on C3: packets for the camera rays, their first bounce and the
 	// camera rays' shadow rays
 	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketClosest1 | rtamd::kPacketShadow0;
@@ -285,12 +286,13 @@ struct Render {
 		auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
 		int64_t so = 0, ho = 0;
 		b.n = static_cast<int32_t>(lv.size());
+		b.all_lights = (s->shadow_all_lights >> (lv.front().first == 0 ? 0 : 1)) & 1;
 		for (int k = 0; k < b.n; k++) {
 			b.level[k] = lv[k].first;
 			b.nh[k] = lv[k].second;
 			b.shadow_begin[k] = so;
 			b.shade_begin[k] = ho;
-			so += nl * wave_up(lv[k].second);  // every light's items start on a wave boundary
+			so += (b.all_lights ? 1 : nl) * wave_up(lv[k].second);  // every light's items start on a wave boundary
 			ho += wave_up(lv[k].second);
 		}
 		b.shadow_begin[b.n] = so;
@@ -485,6 +487,7 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 		s->batch_lanes = std::min(kMaxLanes, std::max(1, std::atoi(bl)));
 	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
+	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));

@@ -12,6 +12,9 @@
 // Acceleration (new design, exact): LBVH per mesh, world-space boxes per geometry, and
 // conservative pre-tests that only ever skip work whose outcome is already decided.
 #pragma once
+#ifndef RT_SPECULATIVE
+#define RT_SPECULATIVE 1
+#endif
 #ifndef RT_PHASE_PROF
 #define RT_PHASE_PROF 0
 #endif
@@ -256,7 +259,7 @@ __device__ __forceinline__ double prune_limit(double best_dist) { return best_di
 //   like the closest-hit search restricted to dist <= prune_cap.
 // The search itself, without the reference's bounding-box gate (see mesh_hit).
 template <bool kAnyHit, typename GP>
-                         __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
+__device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
                          double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
                          DeviceCounters* ctr, WorkStats& ws) {
 	settled = false;
@@ -286,7 +289,11 @@ template <bool kAnyHit, typename GP>
 		int32_t ref = G->bvh_root;
 		int sp = 0;
 		auto pop = [&]() { return sp > 0 ? stack[--sp * kBlock] : (int32_t)-1; };
-		while (ref != -1) {
+		// Speculative (Aila & Laine 2009): a lane that reaches a leaf while other lanes are
+		// still walking inner nodes postpones it (`leaf`) and keeps walking, so fewer lanes
+		// idle in either phase.  Any visiting order selects the same face (test_face).
+		int32_t leaf = -1;
+		while (ref != -1 || leaf != -1) {
 			PROF_BEGIN(tn);
 			while (ref >= 0) {
 				ws.nodes++;
@@ -312,20 +319,35 @@ template <bool kAnyHit, typename GP>
 				} else {
 					ref = pop();
 				}
+				if (RT_SPECULATIVE && ref <= -2 && leaf == -1) {
+					leaf = ref;
+					ref = pop();
+				}
+				if (RT_SPECULATIVE && __ballot(leaf == -1) == 0) break;  // every walking lane holds a leaf
 			}
 			PROF_END(ws, PH_NODES, tn);
-			if (ref == -1) break;
-			const int32_t code = -2 - ref;
-			const int32_t f0 = G->face_begin + (code >> 3), f1 = f0 + (code & 7);
+			if (!RT_SPECULATIVE && ref <= -2) {
+				leaf = ref;
+				ref = pop();
+			}
+			// the postponed leaf, then a leaf the walk stopped on
 			PROF_BEGIN(tf);
-			for (int32_t f = f0; f < f1; f++)
-				if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
-					PROF_END(ws, PH_FACES, tf);
-					settled = true;
-					return true;
+			while (leaf != -1) {
+				const int32_t code = -2 - leaf;
+				const int32_t f0 = G->face_begin + (code >> 3), f1 = f0 + (code & 7);
+				for (int32_t f = f0; f < f1; f++)
+					if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+						PROF_END(ws, PH_FACES, tf);
+						settled = true;
+						return true;
+					}
+				leaf = -1;
+				if (ref <= -2) {
+					leaf = ref;
+					ref = pop();
 				}
+			}
 			PROF_END(ws, PH_FACES, tf);
-			ref = pop();
 		}
 	}
 	found_dist = best.dist;

@@ -98,7 +98,8 @@ struct ShadeBatch {
 	int32_t n;                           // levels in the batch
 	int32_t level[kMaxBatch];
 	int64_t nh[kMaxBatch];               // hits of each level (cur.counts[0])
-	int64_t shadow_begin[kMaxBatch + 1]; // k_shadow item ranges: n_nonambient x nh rounded up to 64 each
+	int32_t all_lights;                  // k_shadow items: 1 = one per hit (all lights), 0 = per (light, hit)
+	int64_t shadow_begin[kMaxBatch + 1]; // k_shadow item ranges: (all_lights ? 1 : n_nonambient) x nh rounded up to 64
 	int64_t shade_begin[kMaxBatch + 1];  // k_shade item ranges: nh each
 };
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,

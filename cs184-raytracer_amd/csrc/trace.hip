@@ -351,9 +351,13 @@ while (k + 1 < B.n && t0 >= begin[k + 1]) k++;
 return BatchItem{B.level[k], t - begin[k], B.nh[k]};
 }
 
-// Shadow rays: item t of a level -> (light j, hit h) with t = j * nh64 + h, nh64 = nh rounded
-// up to a multiple of 64: light-major, and every wave traces rays towards ONE light (its
-// record is read with scalar loads) from neighbouring hits (scene.cpp:87-93).
+// Shadow rays (scene.cpp:87-93), two item layouts (ShadeBatch::all_lights):
+//  - light-major: item t of a level -> (light j, hit h) with t = j * nh64 + h, nh64 = nh
+//    rounded up to a multiple of 64, so every wave traces rays towards ONE light;
+//  - all lights: item t -> hit h = t, and the wave traces the shadow rays of its 64 hits
+//    towards each light in turn (one light at a time, still wave-uniform), loading the hit
+//    records once for all lights.
+// The light record of the wave is read with scalar loads.
 template <bool kPacket>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
@@ -369,35 +373,46 @@ __global__ void __launch_bounds__(kBlock)
 	const int nl = S.n_nonambient;
 	WorkStats ws{};
 	PROF_BEGIN(t_total);
-	const int64_t nh64 = (nh + 63) & ~int64_t(63);
-	// the wave's light: j = t0 / nh64 for its first item t0 (a few scalar steps: nl <= 64)
-	const int64_t t0 = t - (threadIdx.x & 63);
-	int j = 0;
-	while (j + 1 < nl && t0 >= (j + 1) * nh64) j++;
-	j = __builtin_amdgcn_readfirstlane(j);
-	const int64_t h = t - j * nh64;
-	const bool on = h < nh;
-	V3 P = mk(0, 0, 0), Ld = mk(0, 0, 1);
-	bool rev = false;
-	double dL = 0;
-	if (on) {
-	const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
-		P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
-		const V3 N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
-		const bool inside = cur.hinside[h];
-		const bool point = L.kind == DLIGHT_POINT;
-		const V3 lv = load3(L.vec);
-		Ld = ray_dir(point ? lv - P : -lv, ctr);  // Light::calculateRayToLight
-		rev = (dot4z(N, Ld) < 0) ^ inside;
-		dL = point ? sqrt(sq4(lv - P)) : INFINITY;
+	int j0 = 0, j1 = nl;
+	int64_t h = t;
+	if (!B.all_lights) {
+		const int64_t nh64 = (nh + 63) & ~int64_t(63);
+		// the wave's light: j = t0 / nh64 for its first item t0 (a few scalar steps: nl <= 64)
+		const int64_t t0 = t - (threadIdx.x & 63);
+		int j = 0;
+		while (j + 1 < nl && t0 >= (j + 1) * nh64) j++;
+		j0 = __builtin_amdgcn_readfirstlane(j);
+		j1 = j0 + 1;
+		h = t - j0 * nh64;
 	}
-	if (on) PROF_END(ws, PH_SETUP, t_total);
-	bool occ = false;
-	if (kPacket)
-		occ = occluded_packet(S, P, Ld, rev, dL, on, stack, ctr, ws);
-	else if (on)
-		occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
-	if (on) cur.occl[h * S.occl_stride + j] = occ;
+	const bool on = h < nh;
+	V3 P = mk(0, 0, 0), N = mk(0, 0, 1);
+	bool inside = false;
+	if (on) {
+		P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
+		N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
+		inside = cur.hinside[h];
+	}
+	for (int j = j0; j < j1; j++) {
+		V3 Ld = mk(0, 0, 1);
+		bool rev = false;
+		double dL = 0;
+		if (on) {
+			const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
+			const bool point = L.kind == DLIGHT_POINT;
+			const V3 lv = load3(L.vec);
+			Ld = ray_dir(point ? lv - P : -lv, ctr);  // Light::calculateRayToLight
+			rev = (dot4z(N, Ld) < 0) ^ inside;
+			dL = point ? sqrt(sq4(lv - P)) : INFINITY;
+			PROF_END(ws, PH_SETUP, t_total);
+		}
+		bool occ = false;
+		if (kPacket)
+			occ = occluded_packet(S, P, Ld, rev, dL, on, stack, ctr, ws);
+		else if (on)
+			occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
+		if (on) cur.occl[h * S.occl_stride + j] = occ;
+	}
 	if (on) PROF_END(ws, PH_TOTAL, t_total);
 	flush_stats(ws, stats, 1, kPacket);
 }
