@@ -149,7 +149,7 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	}
 	capacity = std::max<int64_t>(capacity, 1024);
 	const int64_t n = capacity;
-	const int64_t nl = std::max(8, s->ds.occl_stride);
+	const int64_t nl = std::max(1, s->ds.n_nonambient);
 	// 18 double arrays, 4 int32 arrays, two flag arrays, n x lights shadow verdicts and the
 	// level's counts, each 256-B aligned
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
@@ -512,7 +512,6 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 		}
 		s->ds.shadow_light[s->ds.n_nonambient++] = static_cast<int32_t>(li);
 	}
-	s->ds.occl_stride = (s->ds.n_nonambient + 7) / 8 * 8;
 	void* c = nullptr;
 	HIP_TRY(hipMalloc(&c, sizeof(rtamd::DeviceCounters)));
 	s->allocs.push_back(c);

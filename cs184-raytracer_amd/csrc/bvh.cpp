@@ -367,7 +367,9 @@ FlatScene flatten_scene(const Scene& s) {
 		// ~10^7 ulps of slack for the fp64 slab and Cramer rounding (validated bit-exact
 		// against the oracle over every shipped scene).  The padded boxes are then
 		// rounded outward to fp32 (DBvhNode).
-		const double pad = 1e-9 * amax + 1e-300;
+		// The node boxes get 2^-18 of amax more: the fp32 node test (intersect.h slab32)
+		// errs by at most ~6 * 2^-24 * amax in position, well inside it.
+		const double pad = (1e-9 + 0x1p-18) * amax + 1e-300;
 		const size_t node_base = fs.nodes.size();
 		for (int attempt = 0; attempt < 2; attempt++) {
 			fs.nodes.resize(node_base);

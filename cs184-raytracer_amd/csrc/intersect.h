@@ -248,6 +248,54 @@ __device__ __forceinline__ V3 safe_inv(V3 d) { return mk(slab_rcp(d.x), slab_rcp
 
 __device__ __forceinline__ double prune_limit(double best_dist) { return best_dist * (1.0 + 4e-9); }
 
+// fp32 node test.  The ray origin is first moved along the ray to where it enters the
+// mesh's box (o' = o + s d, s >= 0; no face lies before it), so |o'| <= amax, the largest
+// vertex coordinate magnitude; then t' = lo * I - o' * I in fp32 errs by at most about
+// 6 * 2^-24 * amax in position, far inside the 2^-18 * amax the node boxes are padded by
+// (bvh.cpp), plus a relative 2^-22 in t' covered by the 2^-20 widening.  A ray that
+// misses the box finds no face whatever the node tests say.  |I| is clamped to 2^60:
+// for a direction component below 2^-60 the clamped distances to the padded planes still
+// exceed any face distance (the planes lie >= 2^-18 amax from every face).
+struct Ray32 {
+	float ix, iy, iz;     // I
+	float oix, oiy, oiz;  // fl32(o') * I
+	double s;             // the shift: t = t' + s
+};
+__device__ __forceinline__ float clamp_inv32(double inv) { return fminf(fmaxf(static_cast<float>(inv), -0x1p60f), 0x1p60f); }
+template <typename GP>
+__device__ __forceinline__ Ray32 ray32(GP G, V3 o, V3 d, V3 inv) {
+	Ray32 r;
+	double tb, s = 0;
+	if (slab(G->bb_min, G->bb_max, o, inv, INFINITY, tb)) s = fmax(tb, 0.0);
+	r.s = s;
+	r.ix = clamp_inv32(inv.x);
+	r.iy = clamp_inv32(inv.y);
+	r.iz = clamp_inv32(inv.z);
+	r.oix = static_cast<float>(o.x + s * d.x) * r.ix;
+	r.oiy = static_cast<float>(o.y + s * d.y) * r.iy;
+	r.oiz = static_cast<float>(o.z + s * d.z) * r.iz;
+	return r;
+}
+// lim - s rounded up to fp32
+__device__ __forceinline__ float limit32(double lim, double s) {
+	const double l = lim - s;
+	float f = static_cast<float>(l);
+	if (static_cast<double>(f) < l) f = __uint_as_float(__float_as_uint(f) + (f > 0.0f ? 1u : (f == 0.0f ? 1u : 0xffffffffu)));
+	return f;
+}
+template <typename P>
+__device__ __forceinline__ bool slab32(P lo, P hi, const Ray32& r, float lim, float& tnear) {
+	const float tx0 = fmaf(lo[0], r.ix, -r.oix), tx1 = fmaf(hi[0], r.ix, -r.oix);
+	const float ty0 = fmaf(lo[1], r.iy, -r.oiy), ty1 = fmaf(hi[1], r.iy, -r.oiy);
+	const float tz0 = fmaf(lo[2], r.iz, -r.oiz), tz1 = fmaf(hi[2], r.iz, -r.oiz);
+	float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+	float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+	tmin = fmaf(-fabsf(tmin), 0x1p-20f, tmin);
+	tmax = fmaf(fabsf(tmax), 0x1p-20f, tmax);
+	tnear = tmin;
+	return tmax >= tmin && tmax >= 0.0f && tmin <= lim;
+}
+
 
 
 // Mesh::calculateIntNormInObjSpace (geometry.cpp:69-126) with an LBVH in place of the
@@ -286,6 +334,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		// two children are hit is pushed (LDS stack, kStackDepth entries per lane).
 		ws.bvh_entries++;
 		const V3 inv = safe_inv(d);
+		const Ray32 r32 = ray32(G, o, d, inv);
 		int32_t ref = G->bvh_root;
 		int sp = 0;
 		auto pop = [&]() { return sp > 0 ? stack[--sp * kBlock] : (int32_t)-1; };
@@ -298,10 +347,10 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 			while (ref >= 0) {
 				ws.nodes++;
 				const DBvhNode* N = S.nodes + ref;
-				double tn0, tn1;
-				const double lim = fmin(prune_limit(best.dist), prune_cap);
-				const bool h0 = slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
-				const bool h1 = slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+				float tn0, tn1;
+				const float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
+				const bool h0 = slab32(N->lo[0], N->hi[0], r32, lim, tn0);
+				const bool h1 = slab32(N->lo[1], N->hi[1], r32, lim, tn1);
 				if (h0 || h1) {
 					const int c = (h0 && h1) ? (tn1 < tn0 ? 1 : 0) : (h1 ? 1 : 0);
 					const int32_t cf = N->first[c], cc = N->count[c];
@@ -583,6 +632,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 		} else {
 			if (live) ws.bvh_entries++;
 			const V3 inv = safe_inv(d);
+			const Ray32 r32 = ray32(G, o, d, inv);
 			const auto nodes = uniform_ptr(S.nodes);
 			int32_t node = uniform_i32(G->bvh_root);
 			int sp = 0;
@@ -590,10 +640,10 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				PROF_BEGIN(tn);
 				const auto N = nodes + node;
 				if (live) ws.nodes++;
-				double tn0 = 0, tn1 = 0;
-				const double lim = fmin(prune_limit(best.dist), prune_cap);
-				const bool h0 = live && slab(N->lo[0], N->hi[0], o, inv, lim, tn0);
-				const bool h1 = live && slab(N->lo[1], N->hi[1], o, inv, lim, tn1);
+				float tn0 = 0, tn1 = 0;
+				const float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
+				const bool h0 = live && slab32(N->lo[0], N->hi[0], r32, lim, tn0);
+				const bool h1 = live && slab32(N->lo[1], N->hi[1], r32, lim, tn1);
 				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
 				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
 				const int first = uniform_i32((2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0);
@@ -603,7 +653,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				for (int k = 0; k < 2; k++) {
 					const int c = first ^ k;
 					bool want = c ? h1 : h0;
-					if (k == 1) want = want && live && (c ? tn1 : tn0) <= fmin(prune_limit(best.dist), prune_cap);
+					if (k == 1) want = want && live && (c ? tn1 : tn0) <= limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 					if (!wave_any(want)) continue;
 					const int32_t cf = uniform_i32(N->first[c]), cc = uniform_i32(N->count[c]);
 					if (cc > 0) {
@@ -614,8 +664,8 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 								settled = true;
 								live = false;
 							}
-							PROF_END(ws, PH_FACES, tf);
-							} else if (next < 0) {
+						PROF_END(ws, PH_FACES, tf);
+					} else if (next < 0) {
 						next = cf;
 					} else if (sp < kStackDepth) {
 						wstack[sp++] = cf;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)

@@ -20,7 +20,6 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	DCamera cam;
 	int32_t n_geoms, n_lights, n_nonambient;
 	int32_t n_may_raise;                      // geometries with DGeom::may_raise
-	int32_t occl_stride;                      // bytes per ray in RayLevel::occl (n_nonambient rounded to 8)
 	int32_t shadow_light[kMaxShadowLights];  // j-th non-ambient light -> light index
 };
 
@@ -36,7 +35,7 @@ struct RayLevel {
 	double *hnx, *hny, *hnz;     // shading normal (flipped if inside, normalised)
 	uint8_t* hinside;            // the ray's inside flag
 	int32_t* hit_list;           // ray index of each hit (order of discovery)
-	uint8_t* occl;               // [hit][non-ambient light] shadow verdicts
+	uint8_t* occl;               // [non-ambient light][hit] shadow verdicts (light j at j * capacity)
 	// node out
 	double *cr, *cg, *cb;        // local colour, overwritten with the final colour by reduce
 	double *kr, *kg, *kb;        // reflective weight (after TIR), valid when child_refl >= 0

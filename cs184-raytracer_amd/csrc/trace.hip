@@ -411,7 +411,7 @@ __global__ void __launch_bounds__(kBlock)
 			occ = occluded_packet(S, P, Ld, rev, dL, on, stack, ctr, ws);
 		else if (on)
 			occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
-		if (on) cur.occl[h * S.occl_stride + j] = occ;
+		if (on) cur.occl[j * cur.capacity + h] = occ;  // light-major: a wave writes 64 adjacent bytes
 	}
 	if (on) PROF_END(ws, PH_TOTAL, t_total);
 	flush_stats(ws, stats, 1, kPacket);
@@ -441,8 +441,6 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	const V3 P = mk(cur.hpx[hs], cur.hpy[hs], cur.hpz[hs]);
 	const V3 N = mk(cur.hnx[hs], cur.hny[hs], cur.hnz[hs]);
 	const DMaterial& M = S.mats[S.geoms[gi].mat];
-	const uint64_t* occ_words = reinterpret_cast<const uint64_t*>(cur.occl + hs * S.occl_stride);
-	uint64_t occ_word = 0;
 	int j = 0;
 	for (int li = 0; li < S.n_lights; li++) {
 		const DLight& L = S.lights[li];
@@ -451,8 +449,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 			for (int k = 0; k < 3; k++) col[k] = col[k] + (1.0 * L.color[k]) * M.ka[k];
 			continue;
 		}
-		if ((j & 7) == 0) occ_word = occ_words[j >> 3];
-		const bool occ = (occ_word >> (8 * (j & 7))) & 0xff;
+		const bool occ = cur.occl[j * cur.capacity + hs];
 		j++;
 		if (occ) continue;
 		const bool point = L.kind == DLIGHT_POINT;
