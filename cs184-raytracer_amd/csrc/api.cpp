@@ -535,6 +535,7 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	in.n_lights = s->ds.n_lights;
 	in.n_faces = static_cast<int64_t>(fs.face_geo.size());
 	in.n_bvh_nodes = static_cast<int64_t>(fs.nodes.size());
+	in.max_bvh_depth = fs.max_bvh_depth;
 	*out = s.release();
 	return RT_OK;
 }

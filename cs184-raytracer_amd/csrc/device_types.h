@@ -22,7 +22,10 @@ constexpr int kLinearFaces = 8;   // meshes up to this size are scanned linearly
 #define RT_LEAF_FACES 4
 #endif
 constexpr int kLeafFaces = RT_LEAF_FACES;  // faces per LBVH leaf
-constexpr int kStackDepth = 32;   // traversal stack entries per lane (LDS); LBVH depth <= 30
+#ifndef RT_STACK_DEPTH
+#define RT_STACK_DEPTH 32
+#endif
+constexpr int kStackDepth = RT_STACK_DEPTH;  // traversal stack entries per lane (LDS); LBVH depth <= kStackDepth - 2
 
 struct alignas(16) DGeom {
 	double fwd[3][4];     // forwardTransform rows

@@ -73,7 +73,7 @@ class rt_counters(ctypes.Structure):
 class rt_scene_info(ctypes.Structure):
     _fields_ = [("n_geometries", ctypes.c_int32), ("n_spheres", ctypes.c_int32), ("n_meshes", ctypes.c_int32),
                 ("n_lights", ctypes.c_int32), ("n_faces", ctypes.c_int64), ("n_bvh_nodes", ctypes.c_int64),
-                ("device_bytes", ctypes.c_int64)]
+                ("device_bytes", ctypes.c_int64), ("max_bvh_depth", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)

@@ -57,6 +57,8 @@ typedef struct rt_scene_info {
 	int64_t n_faces;         /* triangles incl. the two faces of every `tri` line      */
 	int64_t n_bvh_nodes;     /* flattened LBVH nodes over all meshes                  */
 	int64_t device_bytes;    /* HBM held by the uploaded scene                        */
+	int32_t max_bvh_depth;   /* deepest LBVH (root = depth 0)                          */
+	int32_t reserved;
 } rt_scene_info;
 
 /* ---------------------------------------------------------------- device scene */
