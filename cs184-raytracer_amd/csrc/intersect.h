@@ -347,16 +347,18 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 			while (ref >= 0) {
 				ws.nodes++;
 				const DBvhNode* N = S.nodes + ref;
+				// the child references are read with the boxes (one memory round trip per node)
+				const int4 refs = *reinterpret_cast<const int4*>(N->first);  // first[0], first[1], count[0], count[1]
 				float tn0, tn1;
 				const float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 				const bool h0 = slab32(N->lo[0], N->hi[0], r32, lim, tn0);
 				const bool h1 = slab32(N->lo[1], N->hi[1], r32, lim, tn1);
 				if (h0 || h1) {
 					const int c = (h0 && h1) ? (tn1 < tn0 ? 1 : 0) : (h1 ? 1 : 0);
-					const int32_t cf = N->first[c], cc = N->count[c];
+					const int32_t cf = c ? refs.y : refs.x, cc = c ? refs.w : refs.z;
 					const int32_t near_ref = cc > 0 ? -2 - ((cf << 3) | cc) : cf;
 					if (h0 && h1) {
-						const int32_t ff = N->first[c ^ 1], fc = N->count[c ^ 1];
+						const int32_t ff = c ? refs.x : refs.y, fc = c ? refs.z : refs.w;
 						if (sp < kStackDepth) {
 							stack[sp * kBlock] = fc > 0 ? -2 - ((ff << 3) | fc) : ff;
 							sp++;
