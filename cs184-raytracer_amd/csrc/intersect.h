@@ -641,6 +641,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			for (;;) {
 				PROF_BEGIN(tn);
 				const auto N = nodes + node;
+				const int32_t rf0 = N->first[0], rf1 = N->first[1], rc0 = N->count[0], rc1 = N->count[1];
 				if (live) ws.nodes++;
 				float tn0 = 0, tn1 = 0;
 				const float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
@@ -657,7 +658,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					bool want = c ? h1 : h0;
 					if (k == 1) want = want && live && (c ? tn1 : tn0) <= limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 					if (!wave_any(want)) continue;
-					const int32_t cf = uniform_i32(N->first[c]), cc = uniform_i32(N->count[c]);
+					const int32_t cf = uniform_i32(c ? rf1 : rf0), cc = uniform_i32(c ? rc1 : rc0);
 					if (cc > 0) {
 						PROF_BEGIN(tf);
 						const int32_t f0 = G->face_begin + cf;
