@@ -119,8 +119,33 @@ __device__ bool hits_bounding_box(V3 o, V3 d, P mn, P mx) {
 }
 
 // Per-lane work counters (algorithmic bytes/flops of the roofline)
+// (RT_STATS_LDS: the counters live in the block's LDS, one slot per lane, and are bumped
+// with ds_add: five fewer VGPRs in the traversal loops, where every VGPR counts)
+#ifndef RT_STATS_LDS
+#define RT_STATS_LDS 1
+#endif
+enum WorkCounter : int { W_NODES = 0, W_TRIS, W_CANDS, W_SPHERES, W_ENTRIES, W_COUNT };
 struct WorkStats {
-	uint32_t nodes, tris, cands, spheres, bvh_entries;
+#if RT_STATS_LDS
+	uint32_t* c;  // this lane's counters: c[k * kBlock]
+	__device__ __forceinline__ void init(uint32_t* lds) {
+		c = lds + threadIdx.x;
+#pragma unroll
+		for (int k = 0; k < W_COUNT; k++) c[k * kBlock] = 0;
+	}
+	template <int K>
+	__device__ __forceinline__ void inc() { atomicAdd(c + K * kBlock, 1u); }
+	__device__ __forceinline__ uint32_t get(int k) const { return c[k * kBlock]; }
+#else
+	uint32_t c[W_COUNT];
+	__device__ __forceinline__ void init(uint32_t*) {
+#pragma unroll
+		for (int k = 0; k < W_COUNT; k++) c[k] = 0;
+	}
+	template <int K>
+	__device__ __forceinline__ void inc() { c[K]++; }
+	__device__ __forceinline__ uint32_t get(int k) const { return c[k]; }
+#endif
 #if RT_PHASE_PROF
 	uint32_t ph[kPhaseSlots];  // shader-clock cycles per phase while this lane was active
 #endif
@@ -186,7 +211,7 @@ __device__ __forceinline__ bool quotient_surely_above(double num, double den, do
 template <bool kAnyHit, bool kUniform = false>
 __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn, bool reverse,
                                           double any_limit, MeshBest& best, WorkStats& ws) {
-	ws.tris++;
+	ws.inc<W_TRIS>();
 	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	const V3 rhs = o - p0;
@@ -209,7 +234,7 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	const double dist = t * dn;
 	const int32_t id = scene_ptr<kUniform>(S.fid)[f];
 	if (!(dist < best.dist || (dist == best.dist && id < best.id))) return false;
-	ws.cands++;
+	ws.inc<W_CANDS>();
 	const V3 tn = face_normal<kUniform>(S, f, a, b);
 	const bool front = dot4z(tn, d) < 0;
 	if (!front ^ reverse) return false;
@@ -332,7 +357,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		// node and face work do not interleave within a wave.  `ref` >= 0 is a node,
 		// <= -2 a leaf (face offset << 3 | count), -1 done.  The far child of a node whose
 		// two children are hit is pushed (LDS stack, kStackDepth entries per lane).
-		ws.bvh_entries++;
+		ws.inc<W_ENTRIES>();
 		const V3 inv = safe_inv(d);
 		const Ray32 r32 = ray32(G, o, d, inv);
 		int32_t ref = G->bvh_root;
@@ -345,7 +370,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		while (ref != -1 || leaf != -1) {
 			PROF_BEGIN(tn);
 			while (ref >= 0) {
-				ws.nodes++;
+				ws.inc<W_NODES>();
 				const DBvhNode* N = S.nodes + ref;
 				// the child references are read with the boxes (one memory round trip per node)
 				const int4 refs = *reinterpret_cast<const int4*>(N->first);  // first[0], first[1], count[0], count[1]
@@ -505,7 +530,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
-			ws.spheres++;
+			ws.inc<W_SPHERES>();
 			PROF_BEGIN(ts);
 			hit = sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
@@ -547,7 +572,7 @@ __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool rever
 	bool hit, settled = false;
 	double fd;
 	if (G->kind == DGEOM_SPHERE) {
-		ws.spheres++;
+		ws.inc<W_SPHERES>();
 		PROF_BEGIN(ts);
 		hit = sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
@@ -632,7 +657,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				}
 				PROF_END(ws, PH_FACES, tf);
 		} else {
-			if (live) ws.bvh_entries++;
+			if (live) ws.inc<W_ENTRIES>();
 			const V3 inv = safe_inv(d);
 			const Ray32 r32 = ray32(G, o, d, inv);
 			const auto nodes = uniform_ptr(S.nodes);
@@ -642,7 +667,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				PROF_BEGIN(tn);
 				const auto N = nodes + node;
 				const int32_t rf0 = N->first[0], rf1 = N->first[1], rc0 = N->count[0], rc1 = N->count[1];
-				if (live) ws.nodes++;
+				if (live) ws.inc<W_NODES>();
 				float tn0 = 0, tn1 = 0;
 				const float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 				const bool h0 = live && slab32(N->lo[0], N->hi[0], r32, lim, tn0);
@@ -721,7 +746,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
-			if (cand) ws.spheres++;
+			if (cand) ws.inc<W_SPHERES>();
 			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
@@ -769,7 +794,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		bool hit, settled = false;
 		double fd = INFINITY;
 		if (G->kind == DGEOM_SPHERE) {
-			if (cand) ws.spheres++;
+			if (cand) ws.inc<W_SPHERES>();
 			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);

@@ -130,8 +130,8 @@ __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long l
 		if (__lane_id() == 0 && v) atomicAdd(&g_phase[(stage * 2 + packet) * kPhaseSlots + k], v);
 	}
 #endif
-	unsigned long long w[5] = {ws.nodes, ws.tris, ws.cands, ws.spheres, ws.bvh_entries};
-	unsigned long long wmax = ws.nodes;
+	unsigned long long w[5] = {ws.get(W_NODES), ws.get(W_TRIS), ws.get(W_CANDS), ws.get(W_SPHERES), ws.get(W_ENTRIES)};
+	unsigned long long wmax = w[0];
 #pragma unroll
 	for (int k = 0; k < 5; k++)
 		for (int o = 32; o > 0; o >>= 1) w[k] += __shfl_xor(w[k], o);
@@ -194,10 +194,11 @@ template <bool kPacket, typename LV>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
                                              int remaining, const LV& cur, const LV& next,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
-                                             AppendLds& append_lds, int32_t* stack) {
+                                             AppendLds& append_lds, int32_t* stack, uint32_t* stat_lds) {
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
 	WorkStats ws{};
+	ws.init(stat_lds);
 	PROF_BEGIN(t_total);
 	bool hit = false;
 	int gi = -1;
@@ -323,6 +324,7 @@ __global__ void __launch_bounds__(kBlock)
                                                                       DeviceCounters* ctr,
                                                                       unsigned long long* stats) {
 	__shared__ AppendLds append_lds;
+	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
 	// level records read through the constant address space (scalar loads at their uses)
@@ -334,7 +336,8 @@ __global__ void __launch_bounds__(kBlock)
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride)
-		closest_item<kPacket>(S, fg, level, n, remaining, cur, next, ctr, stats, base + threadIdx.x, append_lds, stack);
+		closest_item<kPacket>(S, fg, level, n, remaining, cur, next, ctr, stats, base + threadIdx.x, append_lds, stack,
+		                      stat_lds);
 }
 
 // Level of item t of a batch (wave-uniform: every level's items start on a wave boundary,
@@ -371,7 +374,9 @@ __global__ void __launch_bounds__(kBlock)
 	const int64_t t = it.local, nh = it.nh;
 	const auto& cur = *uniform_ptr(levels + level);
 	const int nl = S.n_nonambient;
+	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
 	WorkStats ws{};
+	ws.init(stat_lds);
 	PROF_BEGIN(t_total);
 	int j0 = 0, j1 = nl;
 	int64_t h = t;
