@@ -494,7 +494,7 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	int rc;
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
-	    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) || (rc = upload(s.get(), fs.face_id, &s->ds.fid)) ||
+	    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) ||
 	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) || (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order))) {
 		rt_scene_destroy(s.release());
 		return rc;

@@ -324,7 +324,7 @@ FlatScene flatten_scene(const Scene& s) {
 			}
 			fs.face_geo.push_back(fg);
 			fs.face_nrm.push_back(fn);
-			fs.face_id.push_back(static_cast<int32_t>(local));
+			fs.face_geo.back().id = static_cast<int32_t>(local);
 		};
 		if (g.face_count <= kLinearFaces) {
 			for (int64_t i = 0; i < g.face_count; i++) emit(i);

@@ -15,7 +15,6 @@ struct FlatScene {
 	std::vector<DLight> lights;
 	std::vector<DFaceGeo> face_geo;
 	std::vector<DFaceNrm> face_nrm;
-	std::vector<int32_t> face_id;
 	std::vector<DBvhNode> nodes;
 	// geometry indices in shadow-test order: the occlusion query is an `any` over the
 	// geometries, so cheap ones (spheres, linearly scanned meshes) go first

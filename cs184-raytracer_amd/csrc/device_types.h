@@ -3,9 +3,9 @@
 // HBM layout (all read-only after rt_scene_create):
 //   DGeom[G]        per-geometry record, insertion order (scene.cpp:147 loop order)
 //   DLight[L]       pre-transformed lights, definition order (scene.cpp:117)
-//   DFaceGeo[F]     per face: p0, va = p1-p0, vb = p2-p0 (object space)      80 B
+//   DFaceGeo[F]     per face: p0, va = p1-p0, vb = p2-p0 (object space) and the face's
+//                   index within its mesh in the reference's order (tie-break)  80 B
 //   DFaceNrm[F]     per face: n0, n1, n2 (object space, w == 0 dropped)       80 B
-//   int32 face_id[F]  face index within its mesh in the reference's order (tie-break)
 //   DBvhNode[N]     flattened binary LBVH, fp32 child boxes stored in the parent  64 B
 // BVH meshes store their faces in LBVH leaf order; small meshes (<= kLinearFaces) keep
 // the reference's order and are scanned linearly exactly like geometry.cpp:78.
@@ -63,7 +63,8 @@ struct alignas(16) DLight {
 
 struct alignas(16) DFaceGeo {
 	double p0[3], va[3], vb[3];
-	double pad;
+	int32_t id;           // the face's index in the reference's order within its mesh (tie-break)
+	int32_t pad;
 };
 
 struct alignas(16) DFaceNrm {

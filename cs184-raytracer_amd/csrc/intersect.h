@@ -214,6 +214,7 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	ws.inc<W_TRIS>();
 	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	const int32_t id = F->id;  // read with the vertices (same 16-B load)
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	if (D == 0) return false;
@@ -232,7 +233,6 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	const double t = Dt / D;
 	if (t < 0) return false;
 	const double dist = t * dn;
-	const int32_t id = scene_ptr<kUniform>(S.fid)[f];
 	if (!(dist < best.dist || (dist == best.dist && id < best.id))) return false;
 	ws.inc<W_CANDS>();
 	const V3 tn = face_normal<kUniform>(S, f, a, b);

@@ -14,7 +14,6 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DLight* lights;
 	const DFaceGeo* fgeo;
 	const DFaceNrm* fnrm;
-	const int32_t* fid;
 	const DBvhNode* nodes;
 	const int32_t* shadow_order;              // geometry order of the occlusion query
 	DCamera cam;
