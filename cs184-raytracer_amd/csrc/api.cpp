@@ -368,10 +368,12 @@ struct Render {
 			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, ln.shade[3]))) return rc;
 		}
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
-		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 0; l--)
+		// colours reduced bottom-up; level 0's reduction is fused into the output
+		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 1; l--)
 			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], ln.levels[l].lv, ln.levels[l + 1].lv, ln.stream));
 		const int64_t W = job.W;
-		HIP_TRY(rtamd::launch_output(ln.n0, ln.levels[0].lv, job.out_rgb_dev ? job.out_rgb_dev + ln.r0 * W * 3 : nullptr,
+		HIP_TRY(rtamd::launch_output(ln.n0, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
+		                             job.out_rgb_dev ? job.out_rgb_dev + ln.r0 * W * 3 : nullptr,
 		                             job.out_rgb8_dev ? job.out_rgb8_dev + ln.r0 * W * 3 : nullptr, job.io, s->stats,
 		                             ln.stream));
 		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));

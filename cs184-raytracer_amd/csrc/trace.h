@@ -105,7 +105,8 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
                         DeviceCounters* ctr, hipStream_t stream);
 hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream);
-hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8_t* out_rgb8,
+// lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output
+hipError_t launch_output(int64_t n, const RayLevel& lvl0, const RayLevel* lvl1, double* out_rgb, uint8_t* out_rgb8,
                          int32_t intersection_only, unsigned long long* stats, hipStream_t stream);
 // End of a render: summary[k] = sum over the shards of statistic k (max for ST_MAX_BITS),
 // summary[ST_COUNT] = the device error word; the shards and the error word are cleared for

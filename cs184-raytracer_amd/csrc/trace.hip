@@ -480,25 +480,31 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 }
 
 // colour = (local + refraction) + reflection * kr, in place (scene.cpp:127,134)
+__device__ __forceinline__ void reduce_colour(int64_t i, const RayLevel& cur, const RayLevel& next, double c[3]) {
+	c[0] = cur.cr[i];
+	c[1] = cur.cg[i];
+	c[2] = cur.cb[i];
+	const int32_t t = cur.child_refr[i], r = cur.child_refl[i];
+	if (t >= 0) {
+		c[0] = c[0] + next.cr[t];
+		c[1] = c[1] + next.cg[t];
+		c[2] = c[2] + next.cb[t];
+	}
+	if (r >= 0) {
+		c[0] = c[0] + next.cr[r] * cur.kr[i];
+		c[1] = c[1] + next.cg[r] * cur.kg[i];
+		c[2] = c[2] + next.cb[r] * cur.kb[i];
+	}
+}
 __global__ void k_reduce(int64_t n, RayLevel cur, RayLevel next) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
-	const int32_t t = cur.child_refr[i], r = cur.child_refl[i];
-	if (t < 0 && r < 0) return;
-	double c0 = cur.cr[i], c1 = cur.cg[i], c2 = cur.cb[i];
-	if (t >= 0) {
-		c0 = c0 + next.cr[t];
-		c1 = c1 + next.cg[t];
-		c2 = c2 + next.cb[t];
-	}
-	if (r >= 0) {
-		c0 = c0 + next.cr[r] * cur.kr[i];
-		c1 = c1 + next.cg[r] * cur.kg[i];
-		c2 = c2 + next.cb[r] * cur.kb[i];
-	}
-	cur.cr[i] = c0;
-	cur.cg[i] = c1;
-	cur.cb[i] = c2;
+	if (cur.child_refr[i] < 0 && cur.child_refl[i] < 0) return;
+	double c[3];
+	reduce_colour(i, cur, next, c);
+	cur.cr[i] = c[0];
+	cur.cg[i] = c[1];
+	cur.cb[i] = c[2];
 }
 
 // writers.cpp:4-9: (uint8)(min(max(v,0),1) * 255), NaN -> 0
@@ -509,15 +515,22 @@ __device__ __forceinline__ uint8_t to_u8(double v) {
 	return (v == v) ? (uint8_t)(int)v : (uint8_t)0;
 }
 
-__global__ void k_output(int64_t n, RayLevel lvl0, double* out, uint8_t* out8, int32_t io, unsigned long long* stats) {
+// the image: level 0's colours, reduced with level 1 on the fly when `reduce` (the last
+// k_reduce fused into the output)
+__global__ void k_output(int64_t n, RayLevel lvl0, RayLevel lvl1, int32_t reduce, double* out, uint8_t* out8, int32_t io,
+                         unsigned long long* stats) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	// level 0's counts were read back; clear them for the lane's next chunk
 	if (i == 0) lvl0.counts[0] = lvl0.counts[1] = 0;
 	double v[3] = {0, 0, 0};
 	if (i < n) {
-		v[0] = lvl0.cr[i];
-		v[1] = lvl0.cg[i];
-		v[2] = lvl0.cb[i];
+		if (reduce) {
+			reduce_colour(i, lvl0, lvl1, v);
+		} else {
+			v[0] = lvl0.cr[i];
+			v[1] = lvl0.cg[i];
+			v[2] = lvl0.cb[i];
+		}
 		if (out) {
 			out[i * 3 + 0] = v[0];
 			out[i * 3 + 1] = v[1];
@@ -639,10 +652,11 @@ hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& n
 	return hipGetLastError();
 }
 
-hipError_t launch_output(int64_t n, const RayLevel& lvl0, double* out_rgb, uint8_t* out_rgb8, int32_t io,
-                         unsigned long long* stats, hipStream_t stream) {
+hipError_t launch_output(int64_t n, const RayLevel& lvl0, const RayLevel* lvl1, double* out_rgb, uint8_t* out_rgb8,
+                         int32_t io, unsigned long long* stats, hipStream_t stream) {
 	if (n <= 0) return hipSuccess;
-	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, lvl0, out_rgb, out_rgb8, io, stats);
+	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, lvl0, lvl1 ? *lvl1 : lvl0,
+	                   lvl1 ? 1 : 0, out_rgb, out_rgb8, io, stats);
 	return hipGetLastError();
 }
 
