@@ -41,10 +41,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N ranks on fewer GPUs)")
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3_bunny_1920x1080_bd4")
-    ap.add_argument("--frames-per-gpu", type=int, default=1,
+    ap.add_argument("--frames-per-gpu", type=int, default=4,
                     help="frames per GPU per step, pipelined over the scene's lanes (rt_render_batch_device)")
     ap.add_argument("--latency-frames", type=int, default=5,
                     help="single-frame renders timed after the run (wall-clock latency of one frame)")
@@ -239,7 +239,7 @@ def main():
             "vs_baseline": None, "dtype": "f64", "data": "synthetic: shipped reference scene data (bunny.obj), "
                                                         "deterministic, no RNG",
             "config": {"workload": a.config, "scene": scene_rel, "width": W, "height": H,
-                       "bounce_depth": kw["bdepth"], "frames_per_step": fps, "frames_in_flight_per_gpu": F,
+                       "bounce_depth": kw["bdepth"], "frames_per_step": fps, "frames_per_gpu_per_step": F,
                        "rays_per_frame": int(rays / a.steps / fps),
                        "ms_per_frame": round(elapsed / a.steps / fps * 1e3, 3),
                        "frame_latency_ms": round(latency * 1e3, 3),

@@ -111,7 +111,7 @@ struct rt_scene {
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
 	int direct_levels = 3;
 	int single_lanes = 1;                        // lanes one frame is split over (RTAMD_LANES)
-	int batch_lanes = 2;                         // frames of a batch in flight (RTAMD_BATCH_LANES)
+	int batch_lanes = 3;                         // frames of a batch in flight (RTAMD_BATCH_LANES)
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)

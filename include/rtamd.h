@@ -124,7 +124,7 @@ int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev
 
 /* A batch of n renders of the scene (params[k] -> out_rgb_dev[k], out_rgb8_dev[k]; either
  * array, or any entry, may be NULL), each equal to its own rt_render_device call.  Up to
- * RTAMD_BATCH_LANES (default 2) images are traced concurrently, so one image's
+ * RTAMD_BATCH_LANES (default 3) images are traced concurrently, so one image's
  * latency-bound deep reflection levels overlap the next image's wide first levels
  * (frame pipelining for throughput; the reference renders one image per renderScene).
  * intersection_only entries are rendered one at a time.  counters: sums over the batch. */
