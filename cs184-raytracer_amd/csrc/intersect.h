@@ -26,7 +26,10 @@
 namespace rtamd {
 namespace dev {
 
-constexpr int kBlock = 128;  // 2 waves; LDS traversal stack = kStackDepth x kBlock x (4 + 4) B
+#ifndef RT_BLOCK
+#define RT_BLOCK 128
+#endif
+constexpr int kBlock = RT_BLOCK;  // threads per traversal block (2 waves); LDS stack = kStackDepth x kBlock x 4 B
 
 
 // Scene data read at a wave-uniform address goes through the constant address space so
