@@ -363,6 +363,8 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		ws.inc<W_ENTRIES>();
 		const V3 inv = safe_inv(d);
 		const Ray32 r32 = ray32(G, o, d, inv);
+		// the node-pruning limit in the shifted fp32 frame; it changes only with best.dist
+		float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 		int32_t ref = G->bvh_root;
 		int sp = 0;
 		auto pop = [&]() { return sp > 0 ? stack[--sp * kBlock] : (int32_t)-1; };
@@ -378,7 +380,6 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 				// the child references are read with the boxes (one memory round trip per node)
 				const int4 refs = *reinterpret_cast<const int4*>(N->first);  // first[0], first[1], count[0], count[1]
 				float tn0, tn1;
-				const float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 				const bool h0 = slab32(N->lo[0], N->hi[0], r32, lim, tn0);
 				const bool h1 = slab32(N->lo[1], N->hi[1], r32, lim, tn1);
 				if (h0 || h1) {
@@ -426,6 +427,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 					ref = pop();
 				}
 			}
+			lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 			PROF_END(ws, PH_FACES, tf);
 		}
 	}
@@ -663,6 +665,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			if (live) ws.inc<W_ENTRIES>();
 			const V3 inv = safe_inv(d);
 			const Ray32 r32 = ray32(G, o, d, inv);
+			float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);  // changes only with best.dist
 			const auto nodes = uniform_ptr(S.nodes);
 			int32_t node = uniform_i32(G->bvh_root);
 			int sp = 0;
@@ -672,7 +675,6 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				const int32_t rf0 = N->first[0], rf1 = N->first[1], rc0 = N->count[0], rc1 = N->count[1];
 				if (live) ws.inc<W_NODES>();
 				float tn0 = 0, tn1 = 0;
-				const float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 				const bool h0 = live && slab32(N->lo[0], N->hi[0], r32, lim, tn0);
 				const bool h1 = live && slab32(N->lo[1], N->hi[1], r32, lim, tn1);
 				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
@@ -684,7 +686,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				for (int k = 0; k < 2; k++) {
 					const int c = first ^ k;
 					bool want = c ? h1 : h0;
-					if (k == 1) want = want && live && (c ? tn1 : tn0) <= limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
+					if (k == 1) want = want && live && (c ? tn1 : tn0) <= lim;
 					if (!wave_any(want)) continue;
 					const int32_t cf = uniform_i32(c ? rf1 : rf0), cc = uniform_i32(c ? rc1 : rc0);
 					if (cc > 0) {
@@ -695,6 +697,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 								settled = true;
 								live = false;
 							}
+						lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 						PROF_END(ws, PH_FACES, tf);
 					} else if (next < 0) {
 						next = cf;
