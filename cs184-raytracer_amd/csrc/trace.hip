@@ -462,7 +462,9 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 		const V3 Ld = ray_dir(point ? lv - P : -lv, ctr);
 		const double nl_dot = dot4z(N, Ld);
 		const double dL = point ? sqrt(sq4(lv - P)) : INFINITY;
-		const double fall = point ? glibc_pow(dL, -L.falloff, log_tab, exp_tab) : 1.0;  // colorForDistance
+		// colorForDistance; glibc's pow(x, +-0) is exactly 1 and pow(x, 1) exactly x (its < 0.52-ulp
+		// bound pins exact results; checked on 500k libm samples), so those exponents skip it
+		const double fall = (point && L.falloff != 0.0) ? glibc_pow(dL, -L.falloff, log_tab, exp_tab) : 1.0;
 		double att[3];
 #pragma unroll
 		for (int k = 0; k < 3; k++) att[k] = point ? fall * L.color[k] : L.color[k];
@@ -470,7 +472,8 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 #pragma unroll
 		for (int k = 0; k < 3; k++) col[k] = col[k] + (diff * att[k]) * M.kd[k];
 		const V3 R = (2 * nl_dot) * N - Ld;
-		const double spec = glibc_pow(max0(-dot4z(d, R)), M.ns, log_tab, exp_tab);
+		const double sbase = max0(-dot4z(d, R));
+		const double spec = M.ns == 1.0 ? sbase : glibc_pow(sbase, M.ns, log_tab, exp_tab);
 #pragma unroll
 		for (int k = 0; k < 3; k++) col[k] = col[k] + (spec * att[k]) * M.ks[k];
 	}

@@ -101,3 +101,19 @@ def test_cli_option_errors_match_reference(args, msg):
     p = subprocess.run([CLI] + args, capture_output=True, text=True)
     assert p.returncode == 1
     assert msg in p.stderr
+
+
+def test_libm_pow_identities_used_by_shading():
+    """k_shade skips pow for exponents -0/+0 (falloff 0) and 1 (ns 1): glibc's pow returns
+    exactly 1 and exactly x there (trace.hip k_shade)."""
+    import ctypes
+    m = ctypes.CDLL("libm.so.6")
+    m.pow.restype = ctypes.c_double
+    m.pow.argtypes = [ctypes.c_double, ctypes.c_double]
+    rng = np.random.default_rng(7)
+    xs = np.concatenate([rng.uniform(0, 1, 20000), np.exp(rng.uniform(-700, 700, 20000)), [0.0, 1.0, np.inf]])
+    for x in xs:
+        x = float(x)
+        assert m.pow(x, 1.0) == x
+        assert m.pow(x, -0.0) == 1.0 and m.pow(x, 0.0) == 1.0
+    assert np.isnan(m.pow(float("nan"), 1.0)) and m.pow(float("nan"), -0.0) == 1.0
