@@ -3,7 +3,13 @@ EXTRA_DEFS=-DRT_PHASE_PROF=1).  Per kernel variant: where the lanes' shader-cloc
 (sums over lanes of the wave's s_memtime deltas while the lane was active).
 
 usage: RTAMD_LIB=cs184-raytracer_amd/rtamd/librtamd_prof.so python tools/phase_profile.py [frames]
-(make -C cs184-raytracer_amd prof builds it)"""
+(make -C cs184-raytracer_amd prof builds it)
+
+Caveat: the shares are lane-weighted and the clock reads perturb scheduling; a phase that
+ends with a memory wait can absorb latency that belongs to later work.  Timing-only
+builds that skip a part ("Where the time goes") are the reliable check:
+e.g. this tool put ~70 % of the level-0 k_shadow in its setup, while skipping the bunny's
+LBVH showed the setup to be ~7 %."""
 import ctypes
 import os
 import sys
