@@ -11,6 +11,9 @@
 #ifndef RT_BVH_SAH
 #define RT_BVH_SAH 1
 #endif
+#ifndef RT_SAH_BINS
+#define RT_SAH_BINS 32
+#endif
 
 namespace rtamd {
 namespace {
@@ -92,7 +95,7 @@ struct Builder {
 	// Binned surface-area-heuristic split of order[b, e) (reorders it in place): the split
 	// between centroid bins minimising area(L) * |L| + area(R) * |R| over the three axes.
 	int sah_split(int b, int e) {
-		constexpr int kBins = 32;
+		constexpr int kBins = RT_SAH_BINS;
 		double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
 		auto centre = [&](int32_t f, int a) { return 0.5 * (boxes[f].lo[a] + boxes[f].hi[a]); };
 		for (int i = b; i < e; i++)
