@@ -178,6 +178,7 @@ def main():
             totals["bytes"][2] += st.pixels * PIXEL_BYTES
             per = lambda xs: [x // F for x in xs]  # the batch's F renders do identical work
             work.update({"trace_rays": st.trace_rays // F, "shadow_rays": st.shadow_rays // F,
+                         "shadow_rays_zero_terms": st.shadow_rays_zero_terms // F,
                          "node_visits": per(st.stage_node_visits), "tri_tests": per(st.stage_tri_tests),
                          "candidates": per(st.stage_candidates), "sphere_tests": per(st.stage_sphere_tests),
                          "bvh_traversals": per(st.stage_bvh_traversals),

@@ -150,10 +150,10 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	capacity = std::max<int64_t>(capacity, 1024);
 	const int64_t n = capacity;
 	const int64_t nl = std::max(1, s->ds.n_nonambient);
-	// 18 double arrays, 4 int32 arrays, two flag arrays, n x lights shadow verdicts and the
+	// 21 double arrays, 4 int32 arrays, two flag arrays, n x lights shadow verdicts and the
 	// level's counts, each 256-B aligned
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	const int64_t bytes = 18 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
+	const int64_t bytes = 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
 	HIP_TRY(hipMalloc(&L.block, bytes));
 	char* p = static_cast<char*>(L.block);
 	auto take = [&](int64_t b) {
@@ -161,8 +161,9 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		p += align(b);
 		return r;
 	};
-	double** d[18] = {&L.lv.ox, &L.lv.oy, &L.lv.oz, &L.lv.dx, &L.lv.dy, &L.lv.dz, &L.lv.hpx, &L.lv.hpy, &L.lv.hpz,
-	                  &L.lv.hnx, &L.lv.hny, &L.lv.hnz, &L.lv.cr, &L.lv.cg, &L.lv.cb, &L.lv.kr, &L.lv.kg, &L.lv.kb};
+	double** d[21] = {&L.lv.ox, &L.lv.oy, &L.lv.oz, &L.lv.dx,  &L.lv.dy,  &L.lv.dz,  &L.lv.hpx,
+	                  &L.lv.hpy, &L.lv.hpz, &L.lv.hnx, &L.lv.hny, &L.lv.hnz, &L.lv.hdx, &L.lv.hdy,
+	                  &L.lv.hdz, &L.lv.cr,  &L.lv.cg,  &L.lv.cb,  &L.lv.kr,  &L.lv.kg,  &L.lv.kb};
 	for (double** q : d) *q = reinterpret_cast<double*>(take(n * 8));
 	L.lv.hgeom = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.hit_list = reinterpret_cast<int32_t*>(take(n * 4));
@@ -626,6 +627,7 @@ int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_coun
 	cnt.shadow_rays = static_cast<int64_t>(sum[rtamd::ST_HITS]) * s->ds.n_nonambient;
 	cnt.reflect_rays = static_cast<int64_t>(sum[rtamd::ST_REFL]);
 	cnt.refract_rays = static_cast<int64_t>(sum[rtamd::ST_REFR]);
+	cnt.shadow_rays_zero_terms = static_cast<int64_t>(sum[rtamd::ST_SHADOW_ZERO]);
 	for (int k = 0; k < 2; k++) {
 		const int b = k ? rtamd::ST_NODES1 : rtamd::ST_NODES0;
 		cnt.stage_node_visits[k] = static_cast<int64_t>(sum[b]);
@@ -678,6 +680,7 @@ void add_counters(rt_counters& a, const rt_counters& b) {
 	a.shadow_rays += b.shadow_rays;
 	a.reflect_rays += b.reflect_rays;
 	a.refract_rays += b.refract_rays;
+	a.shadow_rays_zero_terms += b.shadow_rays_zero_terms;
 	a.pixels += b.pixels;
 	a.intersection_max = std::max(a.intersection_max, b.intersection_max);
 	a.kernel_ms += b.kernel_ms;

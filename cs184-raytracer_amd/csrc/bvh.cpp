@@ -256,6 +256,9 @@ FlatScene flatten_scene(const Scene& s) {
 		}
 		d.falloff = l.falloff;
 		d.kind = l.kind;
+		// colorForDistance (lights.h:24) is the colour itself: finite for every distance
+		d.zero_terms = (l.kind == LIGHT_DIRECTIONAL || (l.kind == LIGHT_POINT && l.falloff == 0.0)) &&
+		               std::isfinite(l.color[0]) && std::isfinite(l.color[1]) && std::isfinite(l.color[2]);
 		fs.lights.push_back(d);
 	}
 	for (const Geometry& g : s.geoms) {
@@ -279,6 +282,9 @@ FlatScene flatten_scene(const Scene& s) {
 		m.ior = g.mat.ior;
 		m.kt_nonzero = !is_zero(g.mat.kt, 3);
 		m.kr_nonzero = !is_zero(g.mat.kr, 3);
+		// pow(+-0, ns) is +-0 only for ns > 0; 0 * kd and 0 * ks are zeros only when finite
+		m.zero_terms = g.mat.ns > 0;
+		for (int k = 0; k < 3; k++) m.zero_terms = m.zero_terms && std::isfinite(g.mat.kd[k]) && std::isfinite(g.mat.ks[k]);
 		d.mat = static_cast<int32_t>(fs.materials.size());
 		fs.materials.push_back(m);
 		if (g.kind == GEOM_SPHERE) {

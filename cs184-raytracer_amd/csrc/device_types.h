@@ -51,6 +51,10 @@ struct alignas(16) DMaterial {   // rtbase.h:30-39
 	double ns, ior;
 	int32_t kt_nonzero;   // !translucencyColor.isZero()  (scene.cpp:115)
 	int32_t kr_nonzero;   // !reflectiveColor.isZero()    (scene.cpp:130)
+	// ns > 0 and kd, ks finite: a light whose diffuse factor max(N.L, 0) and specular base
+	// max(-V.R, 0) are both zero adds exact zeros here (scene.cpp:96-106), whatever the
+	// shadow ray finds (see k_shadow)
+	int32_t zero_terms;
 };
 
 struct alignas(16) DLight {
@@ -58,7 +62,7 @@ struct alignas(16) DLight {
 	double vec[3];        // point position or direction (both after the light's transform)
 	double falloff;
 	int32_t kind;         // 0 point, 1 directional, 2 ambient
-	int32_t pad;
+	int32_t zero_terms;   // attenuated colour finite for every distance: directional, or point with falloff 0
 };
 
 struct alignas(16) DFaceGeo {

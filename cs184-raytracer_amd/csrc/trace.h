@@ -32,7 +32,8 @@ struct RayLevel {
 	// hit records, compacted: entry h (0 <= h < counts[0]) is the h-th hit found, ray hit_list[h]
 	double *hpx, *hpy, *hpz;     // world hit point
 	double *hnx, *hny, *hnz;     // shading normal (flipped if inside, normalised)
-	uint8_t* hinside;            // the ray's inside flag
+	double *hdx, *hdy, *hdz;     // the ray's direction (the viewing ray of the Phong terms)
+	uint8_t* hinside;            // bit 0: the ray's inside flag; bit 1: the material's DMaterial::zero_terms
 	int32_t* hit_list;           // ray index of each hit (order of discovery)
 	uint8_t* occl;               // [non-ambient light][hit] shadow verdicts (light j at j * capacity)
 	// node out
@@ -67,9 +68,10 @@ enum StatSlot : int {
 	ST_NODES1, ST_TRIS1, ST_CANDS1, ST_SPHERES1,   // k_shadow
 	ST_ENTRIES0, ST_ENTRIES1,                      // LBVH traversals started
 	ST_MAXNODES0, ST_MAXNODES1,                    // most node visits of one ray (max)
+	ST_SHADOW_ZERO,                                // shadow rays whose Phong terms are zero (not traced)
 	ST_COUNT
 };
-constexpr int kStatStride = 16;  // u64 per shard (128 B)
+constexpr int kStatStride = 32;  // u64 per shard (256 B)
 
 // Level pipeline.  k_closest(L) finds the closest hits of level L, appends the hits to
 // cur.hit_list (count cur.counts[0]) and spawns the reflection/refraction children into

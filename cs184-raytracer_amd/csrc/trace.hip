@@ -308,7 +308,10 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	cur.hnx[h] = N.x;
 	cur.hny[h] = N.y;
 	cur.hnz[h] = N.z;
-	cur.hinside[h] = inside;
+	cur.hdx[h] = d.x;
+	cur.hdy[h] = d.y;
+	cur.hdz[h] = d.z;
+	cur.hinside[h] = (inside ? 1 : 0) | (S.mats[S.geoms[gi].mat].zero_terms ? 2 : 0);
 	cur.hit_list[h] = (int32_t)i;
 }
 
@@ -392,31 +395,48 @@ __global__ void __launch_bounds__(kBlock)
 	}
 	const bool on = h < nh;
 	V3 P = mk(0, 0, 0), N = mk(0, 0, 1);
-	bool inside = false;
+	bool inside = false, zero_mat = false;
 	if (on) {
 		P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
 		N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
-		inside = cur.hinside[h];
+		const uint8_t fl = cur.hinside[h];
+		inside = fl & 1;
+		zero_mat = fl & 2;
 	}
 	for (int j = j0; j < j1; j++) {
 		V3 Ld = mk(0, 0, 1);
-		bool rev = false;
+		bool rev = false, zero = false;
 		double dL = 0;
 		if (on) {
 			const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
 			const bool point = L.kind == DLIGHT_POINT;
 			const V3 lv = load3(L.vec);
 			Ld = ray_dir(point ? lv - P : -lv, ctr);  // Light::calculateRayToLight
-			rev = (dot4z(N, Ld) < 0) ^ inside;
+			const double nl_dot = dot4z(N, Ld);
+			rev = (nl_dot < 0) ^ inside;
 			dL = point ? sqrt(sq4(lv - P)) : INFINITY;
+			// Both Phong terms of this light (scene.cpp:96-106, the expressions of k_shade)
+			// are exact zeros when max(N.L, 0) and max(-V.R, 0) are (given ns > 0 and finite
+			// colours, DMaterial/DLight::zero_terms): the colour is the same bits whether
+			// the light is occluded or not (it is never -0), so the ray is not traced.
+			if (zero_mat && L.zero_terms && nl_dot <= 0.0) {
+				const V3 R = (2 * nl_dot) * N - Ld;
+				zero = -dot4z(mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]), R) <= 0.0;
+			}
+			// the reference's castRay still maps the ray into every object space (may raise)
+			if (zero) check_may_raise(S, Ld, true, ctr);
 			PROF_END(ws, PH_SETUP, t_total);
 		}
+		const bool trace = on && !zero;
 		bool occ = false;
 		if (kPacket)
-			occ = occluded_packet(S, P, Ld, rev, dL, on, stack, ctr, ws);
-		else if (on)
+			occ = occluded_packet(S, P, Ld, rev, dL, trace, stack, ctr, ws);
+		else if (trace)
 			occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
-		if (on) cur.occl[j * cur.capacity + h] = occ;  // light-major: a wave writes 64 adjacent bytes
+		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
+		if (on) cur.occl[j * cur.capacity + h] = occ || zero;
+		const unsigned long long mz = __ballot(zero);
+		if (mz && __lane_id() == 0) atomicAdd(shard(stats) + ST_SHADOW_ZERO, (unsigned long long)__popcll(mz));
 	}
 	if (on) PROF_END(ws, PH_TOTAL, t_total);
 	flush_stats(ws, stats, 1, kPacket);
@@ -440,9 +460,7 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	const int64_t i = cur.hit_list[hs];
 	const int gi = cur.hgeom[i];
 	double col[3] = {0.0, 0.0, 0.0};
-	V3 o, d;
-	bool inside;
-	level_ray(S, fg, level, i, cur, o, d, inside, ctr);
+	const V3 d = mk(cur.hdx[hs], cur.hdy[hs], cur.hdz[hs]);  // the viewing ray's direction
 	const V3 P = mk(cur.hpx[hs], cur.hpy[hs], cur.hpz[hs]);
 	const V3 N = mk(cur.hnx[hs], cur.hny[hs], cur.hnz[hs]);
 	const DMaterial& M = S.mats[S.geoms[gi].mat];

@@ -67,7 +67,7 @@ class rt_counters(ctypes.Structure):
                 ("stage_launches", ctypes.c_int32 * 3), ("stage_node_visits", ctypes.c_int64 * 2),
                 ("stage_tri_tests", ctypes.c_int64 * 2), ("stage_candidates", ctypes.c_int64 * 2),
                 ("stage_sphere_tests", ctypes.c_int64 * 2), ("stage_bvh_traversals", ctypes.c_int64 * 2),
-                ("stage_max_node_visits", ctypes.c_int64 * 2)]
+                ("stage_max_node_visits", ctypes.c_int64 * 2), ("shadow_rays_zero_terms", ctypes.c_int64)]
 
 
 class rt_scene_info(ctypes.Structure):
@@ -173,6 +173,7 @@ class RenderStats:
     stage_sphere_tests: tuple = ()
     stage_bvh_traversals: tuple = ()
     stage_max_node_visits: tuple = ()
+    shadow_rays_zero_terms: int = 0  # shadow rays decided without traversal (zero Phong terms)
 
     @property
     def rays(self) -> int:
@@ -185,7 +186,8 @@ def _stats(c: rt_counters) -> RenderStats:
                        c.kernel_ms, c.levels, c.trace_launches, c.node_visits, c.tri_tests, c.candidates,
                        c.sphere_tests, tuple(c.stage_ms), tuple(c.stage_launches), tuple(c.stage_node_visits),
                        tuple(c.stage_tri_tests), tuple(c.stage_candidates), tuple(c.stage_sphere_tests),
-                       tuple(c.stage_bvh_traversals), tuple(c.stage_max_node_visits))
+                       tuple(c.stage_bvh_traversals), tuple(c.stage_max_node_visits),
+                       c.shadow_rays_zero_terms)
 
 
 class Scene:

@@ -105,6 +105,9 @@ typedef struct rt_counters {
 	int64_t stage_node_visits[2], stage_tri_tests[2], stage_candidates[2], stage_sphere_tests[2];
 	int64_t stage_bvh_traversals[2];   /* mesh LBVH traversals started (the mesh gate is tested after) */
 	int64_t stage_max_node_visits[2];  /* most LBVH nodes one ray visited (all meshes)       */
+	int64_t shadow_rays_zero_terms;    /* shadow rays (counted in shadow_rays) whose diffuse and
+	                                      specular terms are exact zeros, so the verdict cannot
+	                                      change the colour: decided without traversal         */
 } rt_counters;
 
 /* Scene::renderScene into a caller-owned host buffer of n_rows*W*3 doubles
