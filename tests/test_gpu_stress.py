@@ -121,13 +121,13 @@ def test_zero_phong_terms_lights_behind(gpu, oracle, tmp_path, ns):
     integer exponents, point lights with and without falloff and a directional light, all
     placed so that many hits face away from them."""
     write_soup(tmp_path / "soup.obj", 300, (0, 0, 0), 1.0, seed=7)
-    mat = f"mat   0.01 0.02 0.03   0.5 0.6 0.7   0.8 0.7 0.6 {ns}   0.3 0.3 0.3\n"
+    mat = f"mat   0.01 0.02 0.03   0.5 0.6 0.7   0.8 0.7 0.6 {ns}   0.3 0.3 0.3\n"  # every geometry's
     body = ("cam   0 0 6   -1.5 -1.1 2    1.5 -1.1 2   -1.5 1.1 2   1.5 1.1 2\n"
             "ltp   0 0 -8 0.3 0.3 0.3\n"          # behind everything, no falloff
             "ltp   2 -3 -2 0.4 0.2 0.1 1.5\n"     # behind, with falloff
             "ltd   0.2 -0.3 -1 0.2 0.2 0.2\n"     # directional, pointing towards the camera
             "ltp   -3 3 4 0.2 0.3 0.4\n"          # in front
-            "lta   0.1 0.1 0.1\n" + mat + 'obj   "soup.obj"\n' + MAT_MIRROR +
-            "sph   1.6 0.2 -1.0 0.6\n" + mat + "tri   -4 -1.2 4   4 -1.2 4   4 -1.2 -4\n")
+            "lta   0.1 0.1 0.1\n" + mat + 'obj   "soup.obj"\n' +
+            "sph   1.6 0.2 -1.0 0.6\n" + "tri   -4 -1.2 4   4 -1.2 4   4 -1.2 -4\n")
     st = check(gpu, oracle, scene(tmp_path, "behind", body), w=48, h=36, bdepth=3)
     assert (st.shadow_rays_zero_terms > 0) == (ns > 0)
