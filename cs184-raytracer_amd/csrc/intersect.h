@@ -217,7 +217,13 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	ws.inc<W_TRIS>();
 	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-	const int32_t id = F->id;  // read with the vertices (same 16-B load)
+	// id is fetched with the vertices: the compiler would otherwise issue its load where
+	// it is first used (one more memory round trip per candidate face)
+	const int32_t id = F->id;
+	if constexpr (kUniform)
+		asm volatile("" ::"s"(id));  // materialised here: no separate fetch at its first use
+	else
+		asm volatile("" ::"v"(id));
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	if (D == 0) return false;
@@ -671,12 +677,22 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			int sp = 0;
 			for (;;) {
 				PROF_BEGIN(tn);
+				// the whole 64-B record in one scalar load, both child boxes tested by every
+				// lane (a lane that is done ignores its results): one memory round trip
 				const auto N = nodes + node;
+				float box[2][2][3];  // [child][lo, hi][axis]
+#pragma unroll
+				for (int c = 0; c < 2; c++)
+#pragma unroll
+					for (int a = 0; a < 3; a++) {
+						box[c][0][a] = N->lo[c][a];
+						box[c][1][a] = N->hi[c][a];
+					}
 				const int32_t rf0 = N->first[0], rf1 = N->first[1], rc0 = N->count[0], rc1 = N->count[1];
 				if (live) ws.inc<W_NODES>();
 				float tn0 = 0, tn1 = 0;
-				const bool h0 = live && slab32(N->lo[0], N->hi[0], r32, lim, tn0);
-				const bool h1 = live && slab32(N->lo[1], N->hi[1], r32, lim, tn1);
+				const bool h0 = slab32(box[0][0], box[0][1], r32, lim, tn0) && live;
+				const bool h1 = slab32(box[1][0], box[1][1], r32, lim, tn1) && live;
 				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
 				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
 				const int first = uniform_i32((2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0);

@@ -51,12 +51,14 @@ def scene(tmp_path, name, body):
     return str(f)
 
 
-def check(gpu, oracle, path, w=40, h=30, bdepth=3):
+def check(gpu, oracle, path, w=40, h=30, bdepth=3, bits=False):
     want, cnt = oracle.render(path, w, h, bdepth=bdepth)
     s = gpu.load_scene(path)
     got = s.renderScene(options=gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth))
     st = s.last_stats
     s.close()
+    if bits:  # binary64 bit patterns: NaN payloads and the sign of zero count too
+        got, want = np.ascontiguousarray(got).view(np.uint64), np.ascontiguousarray(want).view(np.uint64)
     diff = int((got != want).any(axis=2).sum())
     assert diff == 0, f"{diff} pixels differ from the oracle"
     assert (st.trace_rays, st.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
@@ -113,15 +115,20 @@ def test_grazing_rays_and_glass(gpu, oracle, tmp_path):
     check(gpu, oracle, scene(tmp_path, "grazing", body), bdepth=6)
 
 
-@pytest.mark.parametrize("ns", [0.0, 0.5, 1.0, 3.0])
-def test_zero_phong_terms_lights_behind(gpu, oracle, tmp_path, ns):
-    """Shadow rays towards lights behind the surface whose diffuse and specular factors are
-    exact zeros are not traced (k_shadow, DMaterial/DLight::zero_terms).  Exercised with
-    ns = 0 (pow(0, 0) = 1: the term is not zero, the ray must be traced), fractional and
-    integer exponents, point lights with and without falloff and a directional light, all
-    placed so that many hits face away from them."""
+KD, KS = "0.5 0.6 0.7", "0.8 0.7 0.6"
+
+
+@pytest.mark.parametrize("kd,ks,ns", [(KD, KS, 0.0), (KD, KS, 0.5), (KD, KS, 1.0), (KD, KS, 3.0), ("0 0 0", KS, 2.0),
+                                      (KD, "0 0 0", 1.0), (KD, "0 0 0", 0.0), ("0 0 0", "0 0 0", 5.0),
+                                      (KD, "0 0 0", -1.0)])
+def test_zero_phong_terms_lights_behind(gpu, oracle, tmp_path, kd, ks, ns):
+    """Shadow rays whose diffuse and specular additions are certain exact zeros are not
+    traced (k_shadow, DMaterial/DLight::zero_terms).  Exercised with ns = 0 (pow(0, 0) = 1:
+    the specular term is not zero), fractional, integer and negative exponents, zero kd or
+    ks, point lights with and without falloff and a directional light, placed so that many
+    hits face away from them.  Compared bit for bit (NaN and -0 included)."""
     write_soup(tmp_path / "soup.obj", 300, (0, 0, 0), 1.0, seed=7)
-    mat = f"mat   0.01 0.02 0.03   0.5 0.6 0.7   0.8 0.7 0.6 {ns}   0.3 0.3 0.3\n"  # every geometry's
+    mat = f"mat   0.01 0.02 0.03   {kd}   {ks} {ns}   0.3 0.3 0.3\n"  # every geometry's
     body = ("cam   0 0 6   -1.5 -1.1 2    1.5 -1.1 2   -1.5 1.1 2   1.5 1.1 2\n"
             "ltp   0 0 -8 0.3 0.3 0.3\n"          # behind everything, no falloff
             "ltp   2 -3 -2 0.4 0.2 0.1 1.5\n"     # behind, with falloff
@@ -129,5 +136,5 @@ def test_zero_phong_terms_lights_behind(gpu, oracle, tmp_path, ns):
             "ltp   -3 3 4 0.2 0.3 0.4\n"          # in front
             "lta   0.1 0.1 0.1\n" + mat + 'obj   "soup.obj"\n' +
             "sph   1.6 0.2 -1.0 0.6\n" + "tri   -4 -1.2 4   4 -1.2 4   4 -1.2 -4\n")
-    st = check(gpu, oracle, scene(tmp_path, "behind", body), w=48, h=36, bdepth=3)
+    st = check(gpu, oracle, scene(tmp_path, "behind", body), w=48, h=36, bdepth=3, bits=True)
     assert (st.shadow_rays_zero_terms > 0) == (ns > 0)
