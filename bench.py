@@ -102,6 +102,28 @@ def cpu_baseline(s, scene, w, h, bdepth, target_s):
         step = max(1, int(step / max(2.0, min(8.0, target_s / max(dt, 1e-3) / 1.5))))
 
 
+def same_algorithm_baseline(scene, w, h, bdepth, target_s):
+    """The HIP path's own algorithm (LBVH, any-hit shadows, zero-term decisions) on this host's
+    cores: oracle/cpu_bvh_cli (bit-exact with the oracle, tests/test_cpu_bvh.py), whole frames
+    until target_s of render time (scene parse and LBVH build excluded) — SURVEY.md H6."""
+    import subprocess
+    cli = os.path.join(REPO, "oracle", "cpu_bvh_cli")
+    if not os.access(cli, os.X_OK):
+        return None
+    cores = _cores()
+    rays, secs, runs = 0, 0.0, 0
+    while secs < target_s and runs < 50:
+        p = subprocess.run([cli, scene, str(w), str(h), str(bdepth), str(cores), "0", str(h), "1", "/dev/null"],
+                           check=True, capture_output=True, text=True)
+        st = json.loads(p.stdout)
+        rays += st["trace_rays"] + st["shadow_rays"]
+        secs += st["render_s"]
+        runs += 1
+    return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"same-algorithm CPU port (oracle/cpu_bvh_cli, {cores} threads: LBVH, any-hit shadows, "
+                      f"zero-term decisions), {runs} whole {w}x{h} frames: {rays} rays in {secs:.1f} s of render time"}
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -263,6 +285,9 @@ def main():
         }
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(s, scene, W, H, kw["bdepth"], a.cpu_seconds)
+            same = same_algorithm_baseline(scene, W, H, kw["bdepth"], a.cpu_seconds / 3)
+            if same:
+                res["cpu_baseline"]["same_algorithm"] = same
         print(json.dumps(res), flush=True)
     s.close()
     if world > 1:
