@@ -109,16 +109,17 @@ struct rt_scene {
 	double* out_dev = nullptr;                   // staging for rt_render
 	int64_t out_capacity = 0;
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
-	int direct_levels = 3;
+	int direct_levels = 2;                       // RTAMD_DIRECT_LEVELS (measured best on C3)
 	int single_lanes = 1;                        // lanes one frame is split over (RTAMD_LANES)
 	int batch_lanes = 3;                         // frames of a batch in flight (RTAMD_BATCH_LANES)
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
 	int shadow_all_lights = 0;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
-	// measured best on C3: packets for the camera rays, their first bounce and the
-	// camera rays' shadow rays
-	int packet_mask = rtamd::kPacketClosest0 | rtamd::kPacketClosest1 | rtamd::kPacketShadow0;
+	// measured best on C3: packets for the camera rays and their first bounce, and
+	// for the shadow rays of both (once the zero-term decision thinned the per-lane waves)
+	int packet_mask =
+	    rtamd::kPacketClosest0 | rtamd::kPacketClosest1 | rtamd::kPacketShadow0 | rtamd::kPacketShadow1;
 };
 
 namespace {
