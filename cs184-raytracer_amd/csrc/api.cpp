@@ -115,7 +115,7 @@ struct rt_scene {
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
-	int shadow_all_lights = 0;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
+	int shadow_all_lights = 1;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// measured best on C3: packets for the camera rays and their first bounce, and
 	// for the shadow rays of both (once the zero-term decision thinned the per-lane waves)
 	int packet_mask =
