@@ -115,6 +115,7 @@ struct rt_scene {
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
+	int fuse_shade = 1;                          // RTAMD_FUSE_SHADE: all-lights k_shadow levels shade in place
 	int shadow_all_lights = 1;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// measured best on C3: packets for the camera rays and their first bounce, and
 	// for the shadow rays of both (once the zero-term decision thinned the per-lane waves)
@@ -304,11 +305,15 @@ struct Render {
 		const auto& ev = ln.level_events[first];
 		HIP_TRY(hipStreamWaitEvent(q, ln.level_events[last][1], 0));
 		HIP_TRY(hipEventRecord(ev[2], q));
+		// one level traced all-lights-per-lane: k_shadow computes the Phong terms itself
+		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(b, s->packet_mask);
 		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) cnt.stage_launches[1]++;
 		HIP_TRY(hipEventRecord(ev[3], q));
-		HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
-		cnt.stage_launches[2]++;
+		if (!b.fused) {
+			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
+			cnt.stage_launches[2]++;
+		}
 		HIP_TRY(hipEventRecord(ev[4], q));
 		ln.shaded.push_back(first);
 		return RT_OK;
@@ -492,6 +497,7 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
+	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));

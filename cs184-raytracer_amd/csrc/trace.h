@@ -99,11 +99,14 @@ struct ShadeBatch {
 	int32_t level[kMaxBatch];
 	int64_t nh[kMaxBatch];               // hits of each level (cur.counts[0])
 	int32_t all_lights;                  // k_shadow items: 1 = one per hit (all lights), 0 = per (light, hit)
+	int32_t fused;                       // all_lights only: k_shadow also computes the Phong terms (no k_shade)
 	int64_t shadow_begin[kMaxBatch + 1]; // k_shadow item ranges: (all_lights ? 1 : n_nonambient) x nh rounded up to 64
 	int64_t shade_begin[kMaxBatch + 1];  // k_shade item ranges: nh each
 };
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
                          unsigned long long* stats, hipStream_t stream, int packet_mask);
+// ShadeBatch::fused may be set only when this holds (the wave-packet all-lights form)
+bool shadow_can_fuse(const ShadeBatch& b, int packet_mask);
 hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
                         DeviceCounters* ctr, hipStream_t stream);
 hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream);

@@ -357,6 +357,52 @@ while (k + 1 < B.n && t0 >= begin[k + 1]) k++;
 return BatchItem{B.level[k], t - begin[k], B.nh[k]};
 }
 
+// Phong terms in light order (scene.cpp:78-108) of hit slot hs (hit point P, shading normal
+// N, viewing direction d); occluded_j(j): the verdict of the j-th non-ambient light.
+template <typename LV, typename OCC>
+__device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, int64_t hs, V3 P, V3 N, V3 d,
+                                          OCC occluded_j, const double* log_tab, const uint64_t* exp_tab,
+                                          DeviceCounters* ctr) {
+	const int64_t i = cur.hit_list[hs];
+	const int gi = cur.hgeom[i];
+	double col[3] = {0.0, 0.0, 0.0};
+	const DMaterial& M = S.mats[S.geoms[gi].mat];
+	int j = 0;
+	for (int li = 0; li < S.n_lights; li++) {
+		const DLight& L = S.lights[li];
+		if (L.kind == DLIGHT_AMBIENT) {
+#pragma unroll
+			for (int k = 0; k < 3; k++) col[k] = col[k] + (1.0 * L.color[k]) * M.ka[k];
+			continue;
+		}
+		const bool occ = occluded_j(j);
+		j++;
+		if (occ) continue;
+		const bool point = L.kind == DLIGHT_POINT;
+		const V3 lv = load3(L.vec);
+		const V3 Ld = ray_dir(point ? lv - P : -lv, ctr);
+		const double nl_dot = dot4z(N, Ld);
+		const double dL = point ? sqrt(sq4(lv - P)) : INFINITY;
+		// colorForDistance; glibc's pow(x, +-0) is exactly 1 and pow(x, 1) exactly x (its < 0.52-ulp
+		// bound pins exact results; checked on 500k libm samples), so those exponents skip it
+		const double fall = (point && L.falloff != 0.0) ? glibc_pow(dL, -L.falloff, log_tab, exp_tab) : 1.0;
+		double att[3];
+#pragma unroll
+		for (int k = 0; k < 3; k++) att[k] = point ? fall * L.color[k] : L.color[k];
+		const double diff = max0(nl_dot);
+#pragma unroll
+		for (int k = 0; k < 3; k++) col[k] = col[k] + (diff * att[k]) * M.kd[k];
+		const V3 R = (2 * nl_dot) * N - Ld;
+		const double sbase = max0(-dot4z(d, R));
+		const double spec = M.ns == 1.0 ? sbase : glibc_pow(sbase, M.ns, log_tab, exp_tab);
+#pragma unroll
+		for (int k = 0; k < 3; k++) col[k] = col[k] + (spec * att[k]) * M.ks[k];
+	}
+	cur.cr[i] = col[0];
+	cur.cg[i] = col[1];
+	cur.cb[i] = col[2];
+}
+
 // Shadow rays (scene.cpp:87-93), two item layouts (ShadeBatch::all_lights):
 //  - light-major: item t of a level -> (light j, hit h) with t = j * nh64 + h, nh64 = nh
 //    rounded up to a multiple of 64, so every wave traces rays towards ONE light;
@@ -403,6 +449,7 @@ __global__ void __launch_bounds__(kBlock)
 		inside = fl & 1;
 		zero_mat = fl & 2;
 	}
+	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
 	for (int j = j0; j < j1; j++) {
 		V3 Ld = mk(0, 0, 1);
 		bool rev = false, zero = false;
@@ -434,12 +481,21 @@ __global__ void __launch_bounds__(kBlock)
 		else if (trace)
 			occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
 		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
-		if (on) cur.occl[j * cur.capacity + h] = occ || zero;
+		if (B.fused)
+			verdicts |= static_cast<unsigned long long>(occ || zero) << j;
+		else if (on)
+			cur.occl[j * cur.capacity + h] = occ || zero;
 		const unsigned long long mz = __ballot(zero);
 		if (mz && __lane_id() == 0) atomicAdd(shard(stats) + ST_SHADOW_ZERO, (unsigned long long)__popcll(mz));
 	}
 	if (on) PROF_END(ws, PH_TOTAL, t_total);
 	flush_stats(ws, stats, 1, kPacket);
+	// fused shading (ShadeBatch::fused: all lights of the hit traced by this lane): the Phong
+	// terms of k_shade from the verdicts in registers
+	if (kPacket && B.fused && on)
+		shade_hit(S, cur, h, P, N, mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]),
+		          [&](int j) { return static_cast<bool>((verdicts >> j) & 1); }, glibc_pow_data::kLogTab,
+		          glibc_pow_data::kExpTab, ctr);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -457,47 +513,11 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	const int level = it.level;
 	const auto& cur = *uniform_ptr(levels + level);
 	const int64_t hs = it.local;  // the hit's slot (hit records, verdicts)
-	const int64_t i = cur.hit_list[hs];
-	const int gi = cur.hgeom[i];
-	double col[3] = {0.0, 0.0, 0.0};
 	const V3 d = mk(cur.hdx[hs], cur.hdy[hs], cur.hdz[hs]);  // the viewing ray's direction
 	const V3 P = mk(cur.hpx[hs], cur.hpy[hs], cur.hpz[hs]);
 	const V3 N = mk(cur.hnx[hs], cur.hny[hs], cur.hnz[hs]);
-	const DMaterial& M = S.mats[S.geoms[gi].mat];
-	int j = 0;
-	for (int li = 0; li < S.n_lights; li++) {
-		const DLight& L = S.lights[li];
-		if (L.kind == DLIGHT_AMBIENT) {
-#pragma unroll
-			for (int k = 0; k < 3; k++) col[k] = col[k] + (1.0 * L.color[k]) * M.ka[k];
-			continue;
-		}
-		const bool occ = cur.occl[j * cur.capacity + hs];
-		j++;
-		if (occ) continue;
-		const bool point = L.kind == DLIGHT_POINT;
-		const V3 lv = load3(L.vec);
-		const V3 Ld = ray_dir(point ? lv - P : -lv, ctr);
-		const double nl_dot = dot4z(N, Ld);
-		const double dL = point ? sqrt(sq4(lv - P)) : INFINITY;
-		// colorForDistance; glibc's pow(x, +-0) is exactly 1 and pow(x, 1) exactly x (its < 0.52-ulp
-		// bound pins exact results; checked on 500k libm samples), so those exponents skip it
-		const double fall = (point && L.falloff != 0.0) ? glibc_pow(dL, -L.falloff, log_tab, exp_tab) : 1.0;
-		double att[3];
-#pragma unroll
-		for (int k = 0; k < 3; k++) att[k] = point ? fall * L.color[k] : L.color[k];
-		const double diff = max0(nl_dot);
-#pragma unroll
-		for (int k = 0; k < 3; k++) col[k] = col[k] + (diff * att[k]) * M.kd[k];
-		const V3 R = (2 * nl_dot) * N - Ld;
-		const double sbase = max0(-dot4z(d, R));
-		const double spec = M.ns == 1.0 ? sbase : glibc_pow(sbase, M.ns, log_tab, exp_tab);
-#pragma unroll
-		for (int k = 0; k < 3; k++) col[k] = col[k] + (spec * att[k]) * M.ks[k];
-	}
-	cur.cr[i] = col[0];
-	cur.cg[i] = col[1];
-	cur.cb[i] = col[2];
+	shade_hit(S, cur, hs, P, N, d, [&](int j) { return static_cast<bool>(cur.occl[j * cur.capacity + hs]); }, log_tab,
+	          exp_tab, ctr);
 }
 
 // colour = (local + refraction) + reflection * kr, in place (scene.cpp:127,134)
@@ -644,12 +664,18 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 	return hipGetLastError();
 }
 
+static bool shadow_packet(const ShadeBatch& b, int packet_mask) {
+	const int lv = b.level[0];
+	return packet_mask & (lv == 0 ? kPacketShadow0 : (lv == 1 && b.n == 1) ? kPacketShadowN | kPacketShadow1 : kPacketShadowN);
+}
+
+bool shadow_can_fuse(const ShadeBatch& b, int packet_mask) { return b.all_lights && shadow_packet(b, packet_mask); }
+
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
                          unsigned long long* stats, hipStream_t stream, int packet_mask) {
 	const int64_t items = b.shadow_begin[b.n];
 	if (items <= 0 || s.n_nonambient <= 0) return hipSuccess;
-	const int lv = b.level[0];
-	if (packet_mask & (lv == 0 ? kPacketShadow0 : (lv == 1 && b.n == 1) ? kPacketShadowN | kPacketShadow1 : kPacketShadowN))
+	if (shadow_packet(b, packet_mask))
 		hipLaunchKernelGGL(k_shadow<true>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, b, levels_dev, ctr,
 		                   stats);
 	else
