@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -13,6 +14,7 @@
 #include "bvh.h"
 #include "scene_host.h"
 #include "trace.h"
+#include "xform.h"
 
 extern "C" int rt_encode_png(const uint8_t* rgb, int width, int height, std::vector<uint8_t>* out);
 
@@ -36,6 +38,7 @@ const char* device_error_text(int code) {  // MathException what() (rtbase.h:14-
 		case rtamd::DERR_NO_DIRECTION: return "ray has no direction";
 		case rtamd::DERR_POINT_DIRECTION: return "ray direction is a point vector";
 		case rtamd::DERR_STACK: return "internal: BVH traversal stack overflow";
+		case rtamd::DERR_ORIGIN_DIRECTION: return "ray origin is a direction vector";
 		default: return "unknown device error";
 	}
 }
@@ -44,7 +47,13 @@ const char* device_error_text(int code) {  // MathException what() (rtbase.h:14-
 
 struct rt_builder {
 	rtamd::Scene scene;
+	// rt_builder_get_desc views (rebuilt on every call)
+	std::vector<rt_geometry_desc> desc_geoms;
+	std::vector<rt_light_desc> desc_lights;
 };
+
+static_assert(sizeof(rt_face_desc) == sizeof(rtamd::Face) && sizeof(rt_face_desc) == 192,
+              "rt_face_desc is Mesh::Face (geometry.h:32) and the host Face");
 
 // One image (or row selection) of a render call: its parameters, outputs and the rows
 // not yet handed to a lane.
@@ -54,6 +63,17 @@ struct Job {
 	uint8_t* out_rgb8_dev;
 	int depth, io;
 	int64_t W, n_rows, chunk_rows, next_row;
+};
+
+// Progress of a render call (scene.cpp:41-44: the calling thread reports completed pixels
+// about every 100 ms): pixels of the chunks whose output kernel has finished, as seen by
+// the host's event polling.
+struct Progress {
+	rt_progress_fn fn = nullptr;
+	void* user = nullptr;
+	int total = 0;
+	int64_t done = 0;
+	double last = -1.0;
 };
 
 struct LevelBuffers {
@@ -106,8 +126,11 @@ struct rt_scene {
 	unsigned long long* stats = nullptr;         // device, kStatShards x kStatStride
 	unsigned long long* summary = nullptr;       // device, ST_COUNT + 1 (k_stats_finish)
 	unsigned long long* summary_host = nullptr;  // pinned mirror
-	double* out_dev = nullptr;                   // staging for rt_render
+	double* out_dev = nullptr;                   // staging for rt_render (f64)
 	int64_t out_capacity = 0;
+	uint8_t* out8_dev = nullptr;                 // staging for rt_render_rgb8
+	int64_t out8_capacity = 0;
+	int fail_after = -1;                         // fault injection (rt_debug_fail_after): launches left
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
 	int direct_levels = 2;                       // RTAMD_DIRECT_LEVELS (measured best on C3)
 	int single_lanes = 1;                        // lanes one frame is split over (RTAMD_LANES)
@@ -256,6 +279,7 @@ struct Render {
 	rt_scene* s;
 	rt_counters cnt{};
 	float kernel_ms = 0.f;
+	Progress* progress = nullptr;
 
 	// k_closest of level L, then the read-back of its counts.  n: the level's ray count, or
 	// with n_dev (the previous level's child counter) an upper bound: the level is queued
@@ -268,6 +292,7 @@ struct Render {
 		if ((rc = ensure_events(ln, L))) return rc;
 		const auto& ev = ln.level_events[L];
 		const rtamd::RayLevel& cur = ln.levels[L].lv;
+		if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
 		// counts start at zero: level 0's are cleared at allocation and by the previous
 		// chunk's k_output, deeper ones by the previous level's k_closest
 		HIP_TRY(hipEventRecord(ev[0], ln.stream));
@@ -409,6 +434,8 @@ struct Render {
 		cnt.levels = std::max<int32_t>(cnt.levels, static_cast<int32_t>(ln.level_n.size()));
 		cnt.pixels += ln.n0;
 		ln.phase = Lane::IDLE;
+		ln.job = nullptr;
+		if (progress) progress->done += ln.n0;
 		return RT_OK;
 	}
 };
@@ -440,6 +467,92 @@ int check_params(const rt_scene* s, const rt_render_params* p) {
 	if (p->bounce_depth < 0) return fail(RT_ERR_ARG, "Bounce depth must be non-negative.");
 	if (p->row_begin < 0 || p->row_end > p->height || p->row_step <= 0 || p->row_begin > p->row_end)
 		return fail(RT_ERR_ARG, "bad row selection");
+	return RT_OK;
+}
+
+// rt_scene_desc -> host scene (the reference's object model, scene.h:35-38): transforms
+// from Eigen's column-major storage, faces verbatim, then the camera corners and lights
+// transformed once (apply_scene_transforms) as the lazy caches of rtbase.h / lights.h would.
+int scene_from_desc(const rt_scene_desc& d, rtamd::Scene& sc) {
+	if (d.n_geometries < 0 || d.n_lights < 0) return fail(RT_ERR_ARG, "negative geometry or light count");
+	if ((d.n_geometries > 0 && !d.geometries) || (d.n_lights > 0 && !d.lights))
+		return fail(RT_ERR_ARG, "null geometry or light array");
+	auto xf = [](const rt_xform_desc& x, rtamd::Affine& fwd, rtamd::Affine& inv, double& det) {
+		fwd = rtamd::affine_from_eigen(x.fwd);
+		if (x.derive) {  // Transformable::forwardTransform(xf): xf.inverse(), determinant()
+			inv = rtamd::affine_inverse(fwd);
+			det = rtamd::affine_det4(fwd);
+		} else {
+			inv = rtamd::affine_from_eigen(x.inv);
+			det = x.det;
+		}
+	};
+	sc = rtamd::Scene{};
+	for (int32_t i = 0; i < d.n_geometries; i++) {
+		const rt_geometry_desc& gd = d.geometries[i];
+		if (gd.kind != RT_GEOM_SPHERE && gd.kind != RT_GEOM_MESH)
+			return fail(RT_ERR_ARG, "geometry " + std::to_string(i) + ": unknown kind");
+		rtamd::Geometry g{};
+		g.kind = gd.kind == RT_GEOM_SPHERE ? rtamd::GEOM_SPHERE : rtamd::GEOM_MESH;
+		xf(gd.xf, g.fwd, g.inv, g.det);
+		const rt_material_desc& m = gd.material;
+		for (int k = 0; k < 3; k++) {
+			g.mat.ka[k] = m.ambient[k];
+			g.mat.kd[k] = m.diffuse[k];
+			g.mat.ks[k] = m.specular[k];
+			g.mat.kr[k] = m.reflective[k];
+			g.mat.kt[k] = m.translucency[k];
+		}
+		g.mat.ns = m.specular_coefficient;
+		g.mat.ior = m.index_of_refractivity;
+		if (g.kind == rtamd::GEOM_SPHERE) {
+			std::memcpy(g.center, gd.center, sizeof(g.center));
+			g.radius = gd.radius;
+		} else {
+			if (gd.n_faces < 0 || (gd.n_faces > 0 && !gd.faces))
+				return fail(RT_ERR_ARG, "geometry " + std::to_string(i) + ": bad face array");
+			g.face_begin = static_cast<int64_t>(sc.faces.size());
+			g.face_count = gd.n_faces;
+			for (int64_t f = 0; f < gd.n_faces; f++) {
+				const rt_face_desc& fd = gd.faces[f];
+				for (int k = 0; k < 3; k++)
+					if (fd.points[k][3] != 1.0)  // the invariant Mesh::updateBoundingBox enforces (geometry.cpp:160-161)
+						return fail(RT_ERR_ARG, "geometry " + std::to_string(i) + ": face point with w != 1");
+				rtamd::Face hf;
+				std::memcpy(&hf, &fd, sizeof(hf));
+				sc.faces.push_back(hf);
+			}
+			std::memcpy(g.bb_min, gd.bbox_min, sizeof(g.bb_min));
+			std::memcpy(g.bb_max, gd.bbox_max, sizeof(g.bb_max));
+			g.box_valid = true;
+		}
+		sc.geoms.push_back(g);
+	}
+	for (int32_t i = 0; i < d.n_lights; i++) {
+		const rt_light_desc& ld = d.lights[i];
+		rtamd::Light l{};
+		if (ld.kind == RT_LIGHT_POINT)
+			l.kind = rtamd::LIGHT_POINT;
+		else if (ld.kind == RT_LIGHT_DIRECTIONAL)
+			l.kind = rtamd::LIGHT_DIRECTIONAL;
+		else if (ld.kind == RT_LIGHT_AMBIENT)
+			l.kind = rtamd::LIGHT_AMBIENT;
+		else
+			return fail(RT_ERR_ARG, "light " + std::to_string(i) + ": unknown kind");
+		l.fwd = rtamd::affine_from_eigen(ld.xf.fwd);
+		std::memcpy(l.color, ld.color, sizeof(l.color));
+		std::memcpy(l.raw, ld.vec, sizeof(l.raw));
+		l.falloff = ld.kind == RT_LIGHT_POINT ? ld.falloff : 0.0;
+		sc.lights.push_back(l);
+	}
+	sc.has_camera = d.has_camera != 0;
+	if (sc.has_camera) {
+		sc.cam_fwd = rtamd::affine_from_eigen(d.camera.xf.fwd);
+		const double* src[5] = {d.camera.eye, d.camera.lower_left, d.camera.lower_right, d.camera.upper_left,
+		                        d.camera.upper_right};
+		for (int k = 0; k < 5; k++) std::memcpy(sc.cam_raw[k], src[k], 4 * sizeof(double));
+	}
+	rtamd::apply_scene_transforms(sc);
 	return RT_OK;
 }
 
@@ -476,16 +589,103 @@ int rt_device_count(void) {
 	return n;
 }
 
+int scene_create(const rtamd::Scene& scene, int device, rt_scene** out);
+
 int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	if (!b || !out) return fail(RT_ERR_ARG, "null builder or output");
+	return scene_create(b->scene, device, out);
+}
+
+int rt_scene_create_desc(const rt_scene_desc* d, int device, rt_scene** out) {
+	if (!d || !out) return fail(RT_ERR_ARG, "null descriptor or output");
 	*out = nullptr;
-	if (!b->scene.has_camera) return fail(RT_ERR_ARG, "At least one camera must be specified.");
+	rtamd::Scene scene;
+	const int rc = scene_from_desc(*d, scene);
+	if (rc) return rc;
+	return scene_create(scene, device, out);
+}
+
+int rt_builder_get_desc(const rt_builder* b, rt_scene_desc* out) {
+	if (!b || !out) return fail(RT_ERR_ARG, "null builder or descriptor");
+	rt_builder* mb = const_cast<rt_builder*>(b);  // the view arrays are builder-owned scratch
+	const rtamd::Scene& sc = b->scene;
+	std::memset(out, 0, sizeof(*out));
+	auto xf = [](const rtamd::Affine& fwd, const rtamd::Affine* inv, double det, rt_xform_desc& x) {
+		std::memset(&x, 0, sizeof(x));
+		rtamd::affine_to_eigen(fwd, x.fwd);
+		if (inv) {
+			rtamd::affine_to_eigen(*inv, x.inv);
+			x.det = det;
+		} else {
+			x.derive = 1;
+		}
+	};
+	mb->desc_geoms.assign(sc.geoms.size(), rt_geometry_desc{});
+	for (size_t i = 0; i < sc.geoms.size(); i++) {
+		const rtamd::Geometry& g = sc.geoms[i];
+		rt_geometry_desc& d = mb->desc_geoms[i];
+		d.kind = g.kind == rtamd::GEOM_SPHERE ? RT_GEOM_SPHERE : RT_GEOM_MESH;
+		xf(g.fwd, &g.inv, g.det, d.xf);
+		const rtamd::Material& m = g.mat;
+		for (int k = 0; k < 3; k++) {
+			d.material.ambient[k] = m.ka[k];
+			d.material.diffuse[k] = m.kd[k];
+			d.material.specular[k] = m.ks[k];
+			d.material.reflective[k] = m.kr[k];
+			d.material.translucency[k] = m.kt[k];
+		}
+		d.material.specular_coefficient = m.ns;
+		d.material.index_of_refractivity = m.ior;
+		std::memcpy(d.center, g.center, sizeof(d.center));
+		d.radius = g.radius;
+		d.n_faces = g.face_count;
+		d.faces = g.face_count ? reinterpret_cast<const rt_face_desc*>(&sc.faces[g.face_begin]) : nullptr;
+		std::memcpy(d.bbox_min, g.bb_min, sizeof(d.bbox_min));
+		std::memcpy(d.bbox_max, g.bb_max, sizeof(d.bbox_max));
+	}
+	mb->desc_lights.assign(sc.lights.size(), rt_light_desc{});
+	for (size_t i = 0; i < sc.lights.size(); i++) {
+		const rtamd::Light& l = sc.lights[i];
+		rt_light_desc& d = mb->desc_lights[i];
+		d.kind = l.kind == rtamd::LIGHT_POINT ? RT_LIGHT_POINT
+		         : l.kind == rtamd::LIGHT_DIRECTIONAL ? RT_LIGHT_DIRECTIONAL : RT_LIGHT_AMBIENT;
+		xf(l.fwd, nullptr, 0.0, d.xf);
+		std::memcpy(d.color, l.color, sizeof(d.color));
+		std::memcpy(d.vec, l.raw, sizeof(d.vec));
+		d.falloff = l.falloff;
+	}
+	out->has_camera = sc.has_camera;
+	out->n_geometries = static_cast<int32_t>(sc.geoms.size());
+	out->n_lights = static_cast<int32_t>(sc.lights.size());
+	if (sc.has_camera) {
+		xf(sc.cam_fwd, nullptr, 0.0, out->camera.xf);
+		double* dst[5] = {out->camera.eye, out->camera.lower_left, out->camera.lower_right, out->camera.upper_left,
+		                  out->camera.upper_right};
+		for (int k = 0; k < 5; k++) std::memcpy(dst[k], sc.cam_raw[k], 4 * sizeof(double));
+	}
+	out->geometries = mb->desc_geoms.empty() ? nullptr : mb->desc_geoms.data();
+	out->lights = mb->desc_lights.empty() ? nullptr : mb->desc_lights.data();
+	return RT_OK;
+}
+
+int rt_builder_set_desc(rt_builder* b, const rt_scene_desc* d) {
+	if (!b || !d) return fail(RT_ERR_ARG, "null builder or descriptor");
+	rtamd::Scene scene;
+	const int rc = scene_from_desc(*d, scene);
+	if (rc) return rc;
+	b->scene = std::move(scene);
+	return RT_OK;
+}
+
+int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
+	*out = nullptr;
+	if (!scene.has_camera) return fail(RT_ERR_ARG, "At least one camera must be specified.");
 	int ndev = 0;
 	if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
 		return fail(RT_ERR_DEVICE, "no HIP device available (the rtamd render path runs only on the GPU)");
 	if (device < 0 || device >= ndev) return fail(RT_ERR_ARG, "bad device index");
 	HIP_TRY(hipSetDevice(device));
-	rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
+	rtamd::FlatScene fs = rtamd::flatten_scene(scene);
 	std::unique_ptr<rt_scene> s(new rt_scene());
 	s->device = device;
 	// tuning knobs; lanes are created on first use
@@ -513,14 +713,14 @@ int rt_scene_create(const rt_builder* b, int device, rt_scene** out) {
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_may_raise = fs.n_may_raise;
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
-	s->ds.n_nonambient = 0;
-	for (size_t li = 0; li < fs.lights.size(); li++) {
-		if (fs.lights[li].kind == rtamd::LIGHT_AMBIENT) continue;
-		if (s->ds.n_nonambient >= rtamd::kMaxShadowLights) {
-			rt_scene_destroy(s.release());
-			return fail(RT_ERR_ARG, "too many non-ambient lights (max 64)");
-		}
-		s->ds.shadow_light[s->ds.n_nonambient++] = static_cast<int32_t>(li);
+	// j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
+	std::vector<int32_t> shadow_light;
+	for (size_t li = 0; li < fs.lights.size(); li++)
+		if (fs.lights[li].kind != rtamd::LIGHT_AMBIENT) shadow_light.push_back(static_cast<int32_t>(li));
+	s->ds.n_nonambient = static_cast<int32_t>(shadow_light.size());
+	if ((rc = upload(s.get(), shadow_light, &s->ds.shadow_light))) {
+		rt_scene_destroy(s.release());
+		return rc;
 	}
 	void* c = nullptr;
 	HIP_TRY(hipMalloc(&c, sizeof(rtamd::DeviceCounters)));
@@ -557,6 +757,7 @@ void rt_scene_destroy(rt_scene* s) {
 	for (auto& ln : s->lanes) lane_destroy(*ln);
 	for (void* p : s->allocs) (void)hipFree(p);
 	if (s->out_dev) (void)hipFree(s->out_dev);
+	if (s->out8_dev) (void)hipFree(s->out8_dev);
 	if (s->summary_host) (void)hipHostFree(s->summary_host);
 	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -576,12 +777,57 @@ namespace {
 // lanes the chunks (of one image, or whole images of a batch) are traced concurrently
 // and one image's latency-bound deep levels overlap another's wide first levels.
 // --intersection-only jobs come one per call (their maximum is a per-image statistic).
-int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters) {
+double now_s() {
+	using clk = std::chrono::steady_clock;
+	return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+
+// After a failed render: nothing of it may outlive the call.  Queued kernels finish (they
+// may still write the caller's buffers, which the caller must not free before this
+// returns), every lane forgets its chunk (its Job lives in the failed call's frame), and
+// the statistics shards and the device error word are cleared for the next render.
+void reset_after_error(rt_scene* s) {
+	(void)hipDeviceSynchronize();
+	for (auto& ln : s->lanes) {
+		ln->phase = Lane::IDLE;
+		ln->job = nullptr;
+		ln->level = 0;
+		ln->level_n.clear();
+		ln->shaded.clear();
+		ln->deferred.clear();
+		for (auto& L : ln->levels)
+			if (L.block) (void)hipMemset(L.lv.counts, 0, 2 * sizeof(int32_t));
+	}
+	(void)hipMemset(s->stats, 0, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride);
+	(void)hipMemset(s->ctr, 0, sizeof(rtamd::DeviceCounters));
+	(void)hipDeviceSynchronize();
+	(void)hipGetLastError();
+}
+
+int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
+                     Progress* progress);
+
+int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
+                Progress* progress = nullptr) {
+	const int rc = render_jobs_impl(s, jobs, caller, counters, progress);
+	// a device MathException is reported after a complete render (nothing in flight, the
+	// statistics already cleared by k_stats_finish); any other error may leave work queued
+	if (rc && rc != RT_ERR_MATH) {
+		const std::string err = g_error;
+		reset_after_error(s);
+		g_error = err;
+	}
+	return rc;
+}
+
+int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
+                     Progress* progress) {
 	const bool batch = jobs.size() > 1;
 	const size_t n_lanes = batch ? std::min<size_t>(jobs.size(), s->batch_lanes) : s->single_lanes;
 	int rc = ensure_lanes(s, n_lanes);
 	if (rc) return rc;
 	Render R{s};
+	R.progress = progress;
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
 	// the caller's stream is joined first (its prior work, e.g. the allocation of the
 	// output buffers, completes before ours starts); the call returns when all is done
@@ -619,6 +865,13 @@ int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_coun
 			if (q != hipSuccess) return fail(RT_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));
 			rc = ln.phase == Lane::TRACING ? R.on_counts(ln) : R.on_done(ln);
 			if (rc) return rc;
+		}
+		if (progress && progress->fn && progress->done < progress->total) {
+			const double t = now_s();
+			if (t - progress->last >= 0.1) {  // scene.cpp:41-44 polls every 100 ms
+				progress->last = t;
+				progress->fn(static_cast<int>(progress->done), progress->total, progress->user);
+			}
 		}
 		if (!busy) break;
 	}
@@ -711,17 +964,31 @@ void add_counters(rt_counters& a, const rt_counters& b) {
 	}
 }
 
-}  // namespace
 
-extern "C" {
-
-int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_dev, void* stream_v,
-                     rt_counters* counters) {
-	return rt_render_batch_device(s, 1, p, &out_rgb_dev, &out_rgb8_dev, stream_v, counters);
+// device staging buffers of rt_render / rt_render_rgb8 (and of --intersection-only renders
+// whose caller wants RGB8 only: the f64 image is needed for the global maximum)
+int ensure_staging(rt_scene* s, int64_t n_pixels, bool f64, bool u8) {
+	if (f64 && s->out_capacity < n_pixels) {
+		if (s->out_dev) HIP_TRY(hipFree(s->out_dev));
+		s->out_dev = nullptr;
+		s->out_capacity = 0;
+		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->out_dev), std::max<int64_t>(n_pixels, 1) * 3 * sizeof(double)));
+		s->out_capacity = n_pixels;
+	}
+	if (u8 && s->out8_capacity < n_pixels) {
+		if (s->out8_dev) HIP_TRY(hipFree(s->out8_dev));
+		s->out8_dev = nullptr;
+		s->out8_capacity = 0;
+		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->out8_dev), std::max<int64_t>(n_pixels, 1) * 3));
+		s->out8_capacity = n_pixels;
+	}
+	return RT_OK;
 }
 
-int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params, double* const* out_rgb_dev,
-                           uint8_t* const* out_rgb8_dev, void* stream_v, rt_counters* counters) {
+bool whole_image(const rt_render_params* p) { return p->row_begin == 0 && p->row_end == p->height && p->row_step == 1; }
+
+int render_batch(rt_scene* s, int n, const rt_render_params* params, double* const* out_rgb_dev,
+                 uint8_t* const* out_rgb8_dev, void* stream_v, rt_counters* counters, Progress* progress) {
 	if (!s || !params || n < 0) return fail(RT_ERR_ARG, "null scene or params");
 	for (int k = 0; k < n; k++) {
 		const int rc = check_params(s, params + k);
@@ -735,7 +1002,7 @@ int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params, d
 	auto flush = [&]() -> int {
 		if (jobs.empty()) return RT_OK;
 		rt_counters c{};
-		const int rc = render_jobs(s, jobs, caller, &c);
+		const int rc = render_jobs(s, jobs, caller, &c, progress);
 		jobs.clear();
 		if (!rc) add_counters(total, c);
 		return rc;
@@ -745,6 +1012,15 @@ int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params, d
 		if (j.n_rows <= 0) continue;
 		int rc;
 		if (j.io) {  // alone: its maximum is its own
+			if (j.out_rgb8_dev && !j.out_rgb_dev) {
+				// RGB8 of an --intersection-only image: normalised by the image's maximum
+				// (scene.cpp:50-58) from an f64 staging image
+				if (!whole_image(j.p))
+					return fail(RT_ERR_ARG, "--intersection-only row subsets need out_rgb (the normalisation "
+					                        "waits for the global maximum, rt_normalize_device)");
+				if ((rc = ensure_staging(s, j.n_rows * j.W, true, false))) return rc;
+				j.out_rgb_dev = s->out_dev;
+			}
 			if ((rc = flush())) return rc;
 			jobs.push_back(j);
 			if ((rc = flush())) return rc;
@@ -758,26 +1034,58 @@ int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params, d
 	return RT_OK;
 }
 
-int rt_render(rt_scene* s, const rt_render_params* p, double* out_rgb, rt_progress_fn progress, void* user,
-              rt_counters* counters) {
+// rt_render / rt_render_rgb8: one image into staging buffers, then one copy to the host;
+// progress as scene.cpp:41-44 (the calling thread, about every 100 ms, then complete)
+int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint8_t* out_rgb8, rt_progress_fn progress,
+                   void* user, rt_counters* counters) {
 	int rc = check_params(s, p);
 	if (rc) return rc;
-	if (!out_rgb) return fail(RT_ERR_ARG, "null output");
+	if (!out_rgb && !out_rgb8) return fail(RT_ERR_ARG, "null output");
+	if (out_rgb8 && p->intersection_only && !whole_image(p))
+		return fail(RT_ERR_ARG, "--intersection-only RGB8 needs the whole image (global maximum)");
 	HIP_TRY(hipSetDevice(s->device));
 	const int64_t n = selected_rows(p) * p->width;
-	if (s->out_capacity < n) {
-		if (s->out_dev) HIP_TRY(hipFree(s->out_dev));
-		s->out_dev = nullptr;
-		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->out_dev), std::max<int64_t>(n, 1) * 3 * sizeof(double)));
-		s->out_capacity = n;
-	}
-	const int total = static_cast<int>(std::min<int64_t>(n, 0x7fffffff));
-	if (progress) progress(0, total, user);
-	rc = rt_render_device(s, p, s->out_dev, nullptr, nullptr, counters);
+	if ((rc = ensure_staging(s, n, out_rgb != nullptr || p->intersection_only, out_rgb8 != nullptr))) return rc;
+	Progress pr;
+	pr.fn = progress;
+	pr.user = user;
+	pr.total = static_cast<int>(std::min<int64_t>(n, 0x7fffffff));
+	pr.last = now_s();
+	if (progress) progress(0, pr.total, user);
+	double* rgb_dev = (out_rgb || p->intersection_only) ? s->out_dev : nullptr;
+	uint8_t* rgb8_dev = out_rgb8 ? s->out8_dev : nullptr;
+	rc = render_batch(s, 1, p, &rgb_dev, &rgb8_dev, nullptr, counters, &pr);
 	if (rc) return rc;
-	HIP_TRY(hipMemcpy(out_rgb, s->out_dev, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
-	if (progress) progress(total, total, user);
+	if (out_rgb) HIP_TRY(hipMemcpy(out_rgb, s->out_dev, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
+	if (out_rgb8) HIP_TRY(hipMemcpy(out_rgb8, s->out8_dev, n * 3, hipMemcpyDeviceToHost));
+	if (progress) progress(pr.total, pr.total, user);
 	return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_dev, void* stream_v,
+                     rt_counters* counters) {
+	return render_batch(s, 1, p, &out_rgb_dev, &out_rgb8_dev, stream_v, counters, nullptr);
+}
+
+int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params, double* const* out_rgb_dev,
+                           uint8_t* const* out_rgb8_dev, void* stream_v, rt_counters* counters) {
+	return render_batch(s, n, params, out_rgb_dev, out_rgb8_dev, stream_v, counters, nullptr);
+}
+
+int rt_render(rt_scene* s, const rt_render_params* p, double* out_rgb, rt_progress_fn progress, void* user,
+              rt_counters* counters) {
+	if (!out_rgb) return fail(RT_ERR_ARG, "null output");
+	return render_to_host(s, p, out_rgb, nullptr, progress, user, counters);
+}
+
+int rt_render_rgb8(rt_scene* s, const rt_render_params* p, uint8_t* out_rgb8, rt_progress_fn progress, void* user,
+                   rt_counters* counters) {
+	if (!out_rgb8) return fail(RT_ERR_ARG, "null output");
+	return render_to_host(s, p, nullptr, out_rgb8, progress, user, counters);
 }
 
 int rt_normalize_device(rt_scene* s, double* rgb_dev, int64_t n_pixels, double max_value, uint8_t* out_rgb8_dev,
@@ -814,18 +1122,58 @@ int rt_debug_phase_profile(int device, unsigned long long* out32) {
 
 int rt_selftest_math(int device, int op, const double* x, const double* y, double* out, int64_t n) {
 	if (n <= 0) return RT_OK;
+	if (!x || !out) return fail(RT_ERR_ARG, "null input or output");
 	HIP_TRY(hipSetDevice(device));
-	double *dx = nullptr, *dy = nullptr, *dout = nullptr;
-	HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dx), n * sizeof(double)));
-	HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dy), n * sizeof(double)));
-	HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dout), n * sizeof(double)));
+	struct DeviceBuffers {  // freed on every exit, error paths included
+		double* p[3] = {nullptr, nullptr, nullptr};
+		~DeviceBuffers() {
+			for (double* q : p)
+				if (q) (void)hipFree(q);
+		}
+	} buf;
+	for (double*& q : buf.p) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q), n * sizeof(double)));
+	double *dx = buf.p[0], *dy = buf.p[1], *dout = buf.p[2];
 	HIP_TRY(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
 	HIP_TRY(hipMemcpy(dy, y ? y : x, n * sizeof(double), hipMemcpyHostToDevice));
 	HIP_TRY(rtamd::launch_selftest_math(op, dx, dy, dout, n, nullptr));
 	HIP_TRY(hipMemcpy(out, dout, n * sizeof(double), hipMemcpyDeviceToHost));
-	(void)hipFree(dx);
-	(void)hipFree(dy);
-	(void)hipFree(dout);
+	return RT_OK;
+}
+
+// Diagnostic (not in rtamd.h): FNV-1a digest of everything rt_scene_create would upload
+// for the builder's scene (flattened geometry, LBVHs, materials, lights, camera), computed
+// on the host only: equal digests = identical device scenes (tests of rt_builder_set_desc).
+int rt_debug_builder_digest(const rt_builder* b, uint64_t* out) {
+	if (!b || !out) return fail(RT_ERR_ARG, "null builder or output");
+	const rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
+	uint64_t h = 1469598103934665603ull;
+	auto mix = [&](const void* p, size_t n) {
+		const unsigned char* c = static_cast<const unsigned char*>(p);
+		for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
+	};
+	auto vec = [&](const auto& v) {
+		const uint64_t n = v.size();
+		mix(&n, sizeof(n));
+		if (n) mix(v.data(), n * sizeof(v[0]));
+	};
+	vec(fs.geoms);
+	vec(fs.materials);
+	vec(fs.lights);
+	vec(fs.face_geo);
+	vec(fs.face_nrm);
+	vec(fs.nodes);
+	vec(fs.shadow_order);
+	mix(&fs.camera, sizeof(fs.camera));
+	*out = h;
+	return RT_OK;
+}
+
+// Diagnostic (not in rtamd.h): the scene's next render fails after `launches` more
+// closest-hit launches, as a device failure in the middle of a render would (tests of the
+// error path: the render after it must be complete and exact).  -1 disables.
+int rt_debug_fail_after(rt_scene* s, int launches) {
+	if (!s) return fail(RT_ERR_ARG, "null scene");
+	s->fail_after = launches;
 	return RT_OK;
 }
 

@@ -249,7 +249,8 @@ FlatScene flatten_scene(const Scene& s) {
 		std::memcpy(fs.camera.ur, s.cam[4], sizeof(double) * 4);
 	}
 	for (const Light& l : s.lights) {
-		DLight d{};
+		DLight d;
+		std::memset(&d, 0, sizeof(d));  // padding too: the scene digest hashes the bytes
 		for (int k = 0; k < 3; k++) {
 			d.color[k] = l.color[k];
 			d.vec[k] = l.vec[k];
@@ -262,7 +263,8 @@ FlatScene flatten_scene(const Scene& s) {
 		fs.lights.push_back(d);
 	}
 	for (const Geometry& g : s.geoms) {
-		DGeom d{};
+		DGeom d;
+		std::memset(&d, 0, sizeof(d));
 		std::memcpy(d.fwd, g.fwd.m, sizeof(d.fwd));
 		std::memcpy(d.inv, g.inv.m, sizeof(d.inv));
 		d.kind = g.kind;
@@ -270,7 +272,8 @@ FlatScene flatten_scene(const Scene& s) {
 		d.bvh_root = -1;
 		d.may_raise = direction_may_vanish(g.inv);
 		fs.n_may_raise += d.may_raise;
-		DMaterial m{};
+		DMaterial m;
+		std::memset(&m, 0, sizeof(m));
 		for (int k = 0; k < 3; k++) {
 			m.ka[k] = g.mat.ka[k];
 			m.kd[k] = g.mat.kd[k];
@@ -321,8 +324,10 @@ FlatScene flatten_scene(const Scene& s) {
 		}
 		auto emit = [&](int64_t local) {
 			const Face& f = s.faces[g.face_begin + local];
-			DFaceGeo fg{};
-			DFaceNrm fn{};
+			DFaceGeo fg;
+			std::memset(&fg, 0, sizeof(fg));
+			DFaceNrm fn;
+			std::memset(&fn, 0, sizeof(fn));
 			for (int k = 0; k < 3; k++) {
 				fg.p0[k] = f.p[0][k];
 				fg.va[k] = f.p[1][k] - f.p[0][k];  // face.points_[1] - face.points_[0] (geometry.cpp:80)

@@ -163,9 +163,14 @@ int main(int argc, char** argv) {
 	p.row_begin = 0;
 	p.row_end = o.height;
 	p.row_step = 1;
-	std::vector<double> img(static_cast<size_t>(o.width) * o.height * 3);
+	// RGB8 quantised on the device (writers.cpp:4-9): only 3 bytes per pixel cross PCIe,
+	// unless the raw f64 image is asked for (--dump-raw)
+	const size_t n = static_cast<size_t>(o.width) * o.height * 3;
+	std::vector<double> img(o.dump_raw.empty() ? 0 : n);
+	std::vector<uint8_t> rgb(n);
 	set_alarm(true);
-	const int rc = rt_render(scene, &p, img.data(), update_progress, nullptr, nullptr);
+	int rc = img.empty() ? rt_render_rgb8(scene, &p, rgb.data(), update_progress, nullptr, nullptr)
+	                     : rt_render(scene, &p, img.data(), update_progress, nullptr, nullptr);
 	set_alarm(false);
 	if (rc == RT_ERR_MATH) {
 		std::cerr << "terminate called after throwing an instance of 'MathException'\n  what():  " << rt_last_error()
@@ -176,15 +181,14 @@ int main(int argc, char** argv) {
 		std::cerr << "Error: " << rt_last_error() << std::endl;
 		return 1;
 	}
-	if (!o.dump_raw.empty()) {
+	if (!img.empty()) {
 		FILE* f = std::fopen(o.dump_raw.c_str(), "wb");
 		if (f) {
 			std::fwrite(img.data(), sizeof(double), img.size(), f);
 			std::fclose(f);
 		}
+		rt_to_rgb8(img.data(), static_cast<int64_t>(o.width) * o.height, rgb.data());
 	}
-	std::vector<uint8_t> rgb(img.size());
-	rt_to_rgb8(img.data(), static_cast<int64_t>(o.width) * o.height, rgb.data());
 	if (rt_write_png(o.output.c_str(), rgb.data(), o.width, o.height)) {
 		std::cerr << "Error: " << rt_last_error() << std::endl;
 		return 1;

@@ -96,6 +96,7 @@ enum DeviceError : int32_t {
 	DERR_NO_DIRECTION = 1,      // "ray has no direction"
 	DERR_POINT_DIRECTION = 2,   // "ray direction is a point vector"
 	DERR_STACK = 3,             // traversal stack overflow (internal)
+	DERR_ORIGIN_DIRECTION = 4,  // "ray origin is a direction vector" (camera eye with w == 0)
 };
 
 }  // namespace rtamd

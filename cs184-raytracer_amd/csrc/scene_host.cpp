@@ -316,10 +316,10 @@ void parse_rti_file(Scene& s, const std::string& path) {
 			mat.ior = p[16];
 		} else if (kind == "cam") {
 			s.has_camera = true;
+			s.cam_fwd = xf;
 			for (int k = 0; k < 5; k++) {
-				double h[4];
-				point(3 * k, h);
-				affine_apply(xf, h, s.cam[k]);
+				point(3 * k, s.cam_raw[k]);
+				affine_apply(xf, s.cam_raw[k], s.cam[k]);
 			}
 		} else if (kind == "sph") {
 			Geometry g = begin_geometry(GEOM_SPHERE);
@@ -337,9 +337,9 @@ void parse_rti_file(Scene& s, const std::string& path) {
 		} else if (kind == "ltp") {
 			Light l{};
 			l.kind = LIGHT_POINT;
-			double h[4];
-			point(0, h);
-			affine_apply(xf, h, l.vec);
+			l.fwd = xf;
+			point(0, l.raw);
+			affine_apply(xf, l.raw, l.vec);
 			color(3, l.color);
 			l.falloff = p[6];
 			s.lights.push_back(l);
@@ -349,16 +349,40 @@ void parse_rti_file(Scene& s, const std::string& path) {
 			const double d[4] = {p[0] / len, p[1] / len, p[2] / len, 0.0};
 			Light l{};
 			l.kind = LIGHT_DIRECTIONAL;
+			l.fwd = xf;
+			std::copy(d, d + 4, l.raw);
 			affine_apply(xf, d, l.vec);
 			color(3, l.color);
 			s.lights.push_back(l);
 		} else if (kind == "lta") {
 			Light l{};
 			l.kind = LIGHT_AMBIENT;
+			l.fwd = xf;
 			color(0, l.color);
 			s.lights.push_back(l);
 		}
 	}
+}
+
+Affine affine_from_eigen(const double cm[16]) {
+	Affine a;
+	for (int i = 0; i < 3; i++)
+		for (int j = 0; j < 4; j++) a.m[i][j] = cm[j * 4 + i];
+	return a;
+}
+
+void affine_to_eigen(const Affine& a, double cm[16]) {
+	for (int j = 0; j < 4; j++) {
+		for (int i = 0; i < 3; i++) cm[j * 4 + i] = a.m[i][j];
+		cm[j * 4 + 3] = j == 3 ? 1.0 : 0.0;  // Affine mode: last row (0 0 0 1)
+	}
+}
+
+void apply_scene_transforms(Scene& s) {
+	if (s.has_camera)
+		for (int k = 0; k < 5; k++) affine_apply(s.cam_fwd, s.cam_raw[k], s.cam[k]);
+	for (Light& l : s.lights)
+		if (l.kind != LIGHT_AMBIENT) affine_apply(l.fwd, l.raw, l.vec);
 }
 
 }  // namespace rtamd

@@ -49,11 +49,15 @@ struct Light {  // lights.h
 	double color[3];
 	double vec[4];      // point: fwd*point (w=1); directional: fwd*direction (w=0)
 	double falloff = 0;
+	Affine fwd;         // the light's forwardTransform (lights.h:31,59)
+	double raw[4];      // PointLight::point_ / DirectionalLight::direction_ before fwd
 };
 
 struct Scene {
 	bool has_camera = false;
 	double cam[5][4];   // fwd*{eye, lowerLeft, lowerRight, upperLeft, upperRight} (rtbase.h:86-95)
+	double cam_raw[5][4];  // the same points before the camera's forwardTransform
+	Affine cam_fwd;
 	std::vector<Geometry> geoms;
 	std::vector<Light> lights;
 	std::vector<Face> faces;
@@ -69,5 +73,12 @@ struct MathError {
 
 // RTIParser(scene).parseFile(path): throws ParseError / MathError.
 void parse_rti_file(Scene& scene, const std::string& path);
+
+// Affine from Eigen's Transform<double,3,Affine> storage (16 doubles, column-major) and back
+Affine affine_from_eigen(const double cm[16]);
+void affine_to_eigen(const Affine& a, double cm[16]);
+// fwd * raw for the camera corners and the lights (Transform * Vector4d in Eigen's order),
+// done once here instead of the reference's lazy caches (rtbase.h:86-95, lights.h:28-33,56-61)
+void apply_scene_transforms(Scene& s);
 
 }  // namespace rtamd

@@ -6,6 +6,8 @@
 
 namespace rtamd {
 
+// lights whose shadow verdicts fit the 64-bit mask of the fused level-0 shading (more
+// lights use the light-major layout and k_shade)
 constexpr int kMaxShadowLights = 64;
 
 struct DeviceScene {  // device pointers (HBM), immutable after upload
@@ -19,7 +21,7 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	DCamera cam;
 	int32_t n_geoms, n_lights, n_nonambient;
 	int32_t n_may_raise;                      // geometries with DGeom::may_raise
-	int32_t shadow_light[kMaxShadowLights];  // j-th non-ambient light -> light index
+	const int32_t* shadow_light;              // j-th non-ambient light -> light index
 };
 
 // One wavefront level of ray records (structure of arrays).

@@ -57,9 +57,18 @@ __device__ __forceinline__ void primary_ray(const DCamera& cam, int r, int c, in
 	double p[4];
 #pragma unroll
 	for (int k = 0; k < 4; k++) p[k] = cF * (rF * cam.lr[k] + rI * cam.ur[k]) + cI * (rF * cam.ll[k] + rI * cam.ul[k]);
-	if (p[3] - cam.eye[3] != 0) raise_error(ctr, DERR_POINT_DIRECTION);
+	// Ray(eye, P - eye) (rtbase.h:7-24): origin check, then isZero() over all four
+	// components, then the w check; the first one that fails throws
+	const double dw = p[3] - cam.eye[3];
+	const V3 dv = mk(p[0] - cam.eye[0], p[1] - cam.eye[1], p[2] - cam.eye[2]);
+	if (cam.eye[3] == 0)
+		raise_error(ctr, DERR_ORIGIN_DIRECTION);
+	else if (is_zero3(dv) && fabs(dw) <= 1e-12)
+		raise_error(ctr, DERR_NO_DIRECTION);
+	else if (dw != 0)
+		raise_error(ctr, DERR_POINT_DIRECTION);
 	o = load3(cam.eye);
-	d = ray_dir(mk(p[0] - cam.eye[0], p[1] - cam.eye[1], p[2] - cam.eye[2]), ctr);
+	d = div3(dv, sqrt(sq4(dv)));
 }
 
 template <typename LV>

@@ -76,6 +76,52 @@ class rt_scene_info(ctypes.Structure):
                 ("device_bytes", ctypes.c_int64), ("max_bvh_depth", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
+class rt_xform_desc(ctypes.Structure):
+    """Transformable (rtbase.h:41-64): Eigen Transform4d storage, column-major."""
+    _fields_ = [("fwd", ctypes.c_double * 16), ("inv", ctypes.c_double * 16), ("det", ctypes.c_double),
+                ("derive", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class rt_material_desc(ctypes.Structure):
+    """Material (rtbase.h:30-39)."""
+    _fields_ = [("ambient", ctypes.c_double * 3), ("diffuse", ctypes.c_double * 3), ("specular", ctypes.c_double * 3),
+                ("reflective", ctypes.c_double * 3), ("specular_coefficient", ctypes.c_double),
+                ("translucency", ctypes.c_double * 3), ("index_of_refractivity", ctypes.c_double)]
+
+
+class rt_face_desc(ctypes.Structure):
+    """Mesh::Face (geometry.h:32)."""
+    _fields_ = [("points", (ctypes.c_double * 4) * 3), ("normals", (ctypes.c_double * 4) * 3)]
+
+
+class rt_geometry_desc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("reserved", ctypes.c_int32), ("xf", rt_xform_desc),
+                ("material", rt_material_desc), ("center", ctypes.c_double * 4), ("radius", ctypes.c_float),
+                ("reserved_f", ctypes.c_float), ("faces", ctypes.POINTER(rt_face_desc)), ("n_faces", ctypes.c_int64),
+                ("bbox_min", ctypes.c_double * 4), ("bbox_max", ctypes.c_double * 4)]
+
+
+class rt_light_desc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("reserved", ctypes.c_int32), ("xf", rt_xform_desc),
+                ("color", ctypes.c_double * 3), ("vec", ctypes.c_double * 4), ("falloff", ctypes.c_double)]
+
+
+class rt_camera_desc(ctypes.Structure):
+    _fields_ = [("xf", rt_xform_desc), ("eye", ctypes.c_double * 4), ("lower_left", ctypes.c_double * 4),
+                ("lower_right", ctypes.c_double * 4), ("upper_left", ctypes.c_double * 4),
+                ("upper_right", ctypes.c_double * 4)]
+
+
+class rt_scene_desc(ctypes.Structure):
+    """Scene (scene.h:35-38) as flat arrays (include/rtamd.h)."""
+    _fields_ = [("has_camera", ctypes.c_int32), ("n_geometries", ctypes.c_int32), ("n_lights", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("camera", rt_camera_desc),
+                ("geometries", ctypes.POINTER(rt_geometry_desc)), ("lights", ctypes.POINTER(rt_light_desc))]
+
+
+RT_GEOM_SPHERE, RT_GEOM_MESH = 0, 1
+RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AMBIENT = 0, 1, 2
+
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 
 _lib: Optional[ctypes.CDLL] = None
@@ -107,7 +153,14 @@ def lib() -> ctypes.CDLL:
         "rt_scene_destroy": (None, [vp]),
         "rt_scene_get_info": (i32, [vp, ctypes.POINTER(rt_scene_info)]),
         "rt_render": (i32, [vp, ctypes.POINTER(rt_render_params), vp, PROGRESS_FN, vp, ctypes.POINTER(rt_counters)]),
+        "rt_render_rgb8": (i32, [vp, ctypes.POINTER(rt_render_params), vp, PROGRESS_FN, vp,
+                                 ctypes.POINTER(rt_counters)]),
         "rt_render_device": (i32, [vp, ctypes.POINTER(rt_render_params), vp, vp, vp, ctypes.POINTER(rt_counters)]),
+        "rt_builder_get_desc": (i32, [vp, ctypes.POINTER(rt_scene_desc)]),
+        "rt_builder_set_desc": (i32, [vp, ctypes.POINTER(rt_scene_desc)]),
+        "rt_scene_create_desc": (i32, [ctypes.POINTER(rt_scene_desc), i32, ctypes.POINTER(vp)]),
+        "rt_debug_builder_digest": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
+        "rt_debug_fail_after": (i32, [vp, i32]),
         "rt_render_batch_device": (i32, [vp, i32, ctypes.POINTER(rt_render_params), ctypes.POINTER(vp),
                                          ctypes.POINTER(vp), vp, ctypes.POINTER(rt_counters)]),
         "rt_normalize_device": (i32, [vp, vp, i64, dbl, vp, vp]),
@@ -271,6 +324,55 @@ class Scene:
                                ctypes.byref(cnt)))
         self.last_stats = _stats(cnt)
         return output
+
+    def render_rgb8(self, options: Optional[Options] = None, rows: Optional[tuple] = None,
+                    phandler: Optional[Callable[[int, int], None]] = None, chunk_pixels: int = 0) -> np.ndarray:
+        """rt_render_rgb8: renderScene + convertToRGBImage (writers.cpp:4-9) quantised on the device;
+        returns a uint8 (n_rows, W, 3) array."""
+        o = options or programOptions
+        W, H = o.renderWidth_, o.renderHeight_
+        rb, re_, rs = rows if rows is not None else (0, H, 1)
+        n_rows = max(0, -(-(re_ - rb) // rs))
+        out = np.empty((n_rows, W, 3), dtype=np.uint8)
+        prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels)
+        cb = PROGRESS_FN((lambda c, t, u: phandler(c, t)) if phandler else (lambda c, t, u: None))
+        cnt = rt_counters()
+        _raise(lib().rt_render_rgb8(self.handle, ctypes.byref(prm), out.ctypes.data_as(ctypes.c_void_p), cb, None,
+                                    ctypes.byref(cnt)))
+        self.last_stats = _stats(cnt)
+        return out
+
+    def desc(self) -> rt_scene_desc:
+        """rt_builder_get_desc: the parsed scene as a flat descriptor (views into the builder,
+        valid while this Scene lives and parses nothing more)."""
+        d = rt_scene_desc()
+        _raise(lib().rt_builder_get_desc(self._b, ctypes.byref(d)))
+        return d
+
+    def set_desc(self, d: rt_scene_desc) -> None:
+        """rt_builder_set_desc: replace the (not yet uploaded) scene by a descriptor's."""
+        if self._scene:
+            raise ArgumentError("scene already uploaded")
+        _raise(lib().rt_builder_set_desc(self._b, ctypes.byref(d)))
+
+    @classmethod
+    def from_desc(cls, d: rt_scene_desc, device: int = 0) -> "Scene":
+        """rt_scene_create_desc: a device scene straight from a descriptor (no builder scene)."""
+        s = cls(device)
+        p = ctypes.c_void_p()
+        _raise(lib().rt_scene_create_desc(ctypes.byref(d), device, ctypes.byref(p)))
+        s._scene = p
+        return s
+
+    def digest(self) -> int:
+        """Host-side digest of the device scene rt_scene_create would upload (diagnostic)."""
+        h = ctypes.c_uint64()
+        _raise(lib().rt_debug_builder_digest(self._b, ctypes.byref(h)))
+        return h.value
+
+    def debug_fail_after(self, launches: int) -> None:
+        """Fault injection: the next render fails after `launches` closest-hit launches."""
+        _raise(lib().rt_debug_fail_after(self.handle, launches))
 
     def render_device(self, params: rt_render_params, out_rgb_ptr: int = 0, out_rgb8_ptr: int = 0,
                       stream_ptr: int = 0) -> RenderStats:

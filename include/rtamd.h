@@ -61,12 +61,95 @@ typedef struct rt_scene_info {
 	int32_t reserved;
 } rt_scene_info;
 
+/* ---------------------------------------------------------------- flat scene descriptor */
+/* The reference's in-memory Scene (scene.h:35-38) as plain arrays, for a caller that
+ * already holds one (e.g. Scene::renderScene itself): no file, no
+ * re-parse.  Every field is a member the reference's objects hold, in its own layout:
+ *   - transforms are Eigen's Transform<double,3,Affine> storage, 16 doubles column-major
+ *     (Transformable::forwardTransform().data(), rtbase.h:41-64);
+ *   - Mesh faces are Mesh::Face verbatim (geometry.h:32: std::array<Vector4d,3> points_,
+ *     normals_ = 24 doubles, 192 B), so mesh->faces_.data() can be passed as is;
+ *   - camera corners and light vectors are the UNtransformed points/directions given to
+ *     the setters (rtbase.h:69-73, lights.h:26,54): the library applies forwardTransform()
+ *     once, in Eigen's order, instead of the reference's lazy (racy) caches. */
+enum { RT_GEOM_SPHERE = 0, RT_GEOM_MESH = 1 };
+enum { RT_LIGHT_POINT = 0, RT_LIGHT_DIRECTIONAL = 1, RT_LIGHT_AMBIENT = 2 };
+
+typedef struct rt_xform_desc {      /* Transformable (rtbase.h:41-64)                        */
+	double fwd[16];                 /* forwardTransform().data(), column-major 4x4          */
+	double inv[16];                 /* inverseTransform().data()                             */
+	double det;                     /* transformDeterminant()                                */
+	int32_t derive;                 /* 1: inv and det are derived from fwd here, exactly as
+	                                   Transformable::forwardTransform(xf) does (rtbase.h:51-54) */
+	int32_t reserved;
+} rt_xform_desc;
+
+typedef struct rt_material_desc {   /* Material (rtbase.h:30-39), same field order           */
+	double ambient[3], diffuse[3], specular[3], reflective[3];
+	double specular_coefficient;
+	double translucency[3];
+	double index_of_refractivity;
+} rt_material_desc;
+
+typedef struct rt_face_desc {       /* Mesh::Face (geometry.h:32), object space; point w == 1 */
+	double points[3][4];
+	double normals[3][4];
+} rt_face_desc;
+
+typedef struct rt_geometry_desc {   /* Geometry (geometry.h:6-14)                            */
+	int32_t kind;                   /* RT_GEOM_SPHERE (Sphere) or RT_GEOM_MESH (Mesh)        */
+	int32_t reserved;
+	rt_xform_desc xf;
+	rt_material_desc material;      /* Geometry::material_                                   */
+	double center[4];               /* Sphere::center_                                       */
+	float radius;                   /* Sphere::radius_ (float, geometry.h:22)                */
+	float reserved_f;
+	const rt_face_desc* faces;      /* Mesh::faces_.data()                                   */
+	int64_t n_faces;                /* Mesh::faces_.size()                                   */
+	double bbox_min[4], bbox_max[4]; /* Mesh::boundingBoxMin_/Max_ (geometry.h:35-36): zero
+	                                   unless Mesh::updateBoundingBox ran (obj meshes)        */
+} rt_geometry_desc;
+
+typedef struct rt_light_desc {      /* Light (lights.h:3-75)                                 */
+	int32_t kind;                   /* RT_LIGHT_POINT / _DIRECTIONAL / _AMBIENT              */
+	int32_t reserved;
+	rt_xform_desc xf;               /* only forwardTransform() is used (lights.h:31,59)      */
+	double color[3];                /* Light::color_                                         */
+	double vec[4];                  /* PointLight::point_ / DirectionalLight::direction_      */
+	double falloff;                 /* PointLight::falloffExponent_                          */
+} rt_light_desc;
+
+typedef struct rt_camera_desc {     /* Camera (rtbase.h:66-103)                              */
+	rt_xform_desc xf;
+	double eye[4], lower_left[4], lower_right[4], upper_left[4], upper_right[4];
+} rt_camera_desc;
+
+typedef struct rt_scene_desc {      /* Scene (scene.h:35-38)                                 */
+	int32_t has_camera;             /* Scene::hasCamera()                                    */
+	int32_t n_geometries;
+	int32_t n_lights;
+	int32_t reserved;
+	rt_camera_desc camera;
+	const rt_geometry_desc* geometries;  /* Scene::geometries_, insertion order (scene.cpp:147) */
+	const rt_light_desc* lights;         /* Scene::lights_, definition order (scene.cpp:78)    */
+} rt_scene_desc;
+
+/* A parsed scene as a descriptor: views into the builder's memory, valid until the builder
+ * is destroyed or parses another file (the transforms are those the parser computed). */
+int rt_builder_get_desc(const rt_builder* b, rt_scene_desc* out);
+/* Replaces the builder's scene by a copy of the descriptor's (the host scene that
+ * rt_scene_create_desc uploads). */
+int rt_builder_set_desc(rt_builder* b, const rt_scene_desc* d);
+
 /* ---------------------------------------------------------------- device scene */
 typedef struct rt_scene rt_scene;
 
 /* Builds the per-mesh LBVHs and uploads geometry, materials, lights and camera to
  * HBM of HIP device `device` once; the scene is immutable afterwards. */
 int rt_scene_create(const rt_builder* b, int device, rt_scene** out);
+/* The same from a flat descriptor (the caller's own Scene, no file): equal to
+ * rt_builder_set_desc + rt_scene_create.  The descriptor may be freed on return. */
+int rt_scene_create_desc(const rt_scene_desc* d, int device, rt_scene** out);
 void rt_scene_destroy(rt_scene* s);
 int rt_scene_get_info(const rt_scene* s, rt_scene_info* info);
 
@@ -117,6 +200,13 @@ typedef struct rt_counters {
  * returned with counters->intersection_max for the caller's global reduction. */
 int rt_render(rt_scene* s, const rt_render_params* p, double* out_rgb,
               rt_progress_fn progress, void* user, rt_counters* counters);
+
+/* Scene::renderScene + PNGWriter::convertToRGBImage (writers.cpp:4-9) into a caller-owned
+ * host buffer of n_rows*W*3 bytes: the image is quantised on the device and only the RGB8
+ * bytes cross PCIe (an eighth of rt_render's f64 copy).  --intersection-only needs the
+ * whole image here (the global maximum normalises it first). */
+int rt_render_rgb8(rt_scene* s, const rt_render_params* p, uint8_t* out_rgb8,
+                   rt_progress_fn progress, void* user, rt_counters* counters);
 
 /* Same, with outputs in device memory (either may be NULL): out_rgb_dev (n_rows*W*3
  * doubles) and out_rgb8_dev (n_rows*W*3 bytes, writers.cpp:4-9 quantisation fused).

@@ -1,0 +1,179 @@
+"""GPU tests of the C-ABI entry points added around the render path (round 2).
+
+- rt_scene_create_desc: a scene handed over as rt_scene_desc (the caller's own Scene,
+  scene.h:35-38) renders bit-exactly like the parsed files (reference goldens);
+- rt_render_rgb8: RGB8 quantised on the device equals convertToRGBImage of the f64 image;
+- progress: reported from the calling thread, monotone, ending at the total (scene.cpp:41-44);
+- any number of lights (scene.cpp:77-108 has no limit);
+- a render that fails midway leaves nothing behind: the next render is exact;
+- --intersection-only with an RGB8-only output is normalised by the global maximum.
+Every image is compared bit for bit with the reference's goldens or the pinned oracle.
+"""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from cases import OPTION_SETS, REPO, SCENES, option_kwargs, scene_files
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("scene", scene_files())
+def test_descriptor_scene_matches_reference(gpu, golden, scene):
+    """rt_builder_get_desc -> rt_scene_create_desc -> render == the reference's image."""
+    name, w, h, flags = OPTION_SETS[0]
+    ref = golden["cases"][f"{scene}|{name}"]
+    if ref["rc"] != 0:
+        pytest.skip("scene rejected by the reference")
+    src = gpu.load_scene(os.path.join(SCENES, scene))
+    s = gpu.Scene.from_desc(src.desc())
+    kw = option_kwargs(flags)
+    o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=kw["bdepth"], intersectionOnly_=kw["intersection_only"])
+    img = s.renderScene(options=o)
+    assert sha(img) == ref["f64_sha256"]
+    s.close()
+    src.close()
+
+
+def test_native_descriptor_render(gpu, oracle, tmp_path):
+    """tests/native/desc_check.cpp on the GPU: the in-memory descriptor and the equivalent
+    files render identical f64 and RGB8 images, and both equal the oracle's render."""
+    exe = tmp_path / "desc_check"
+    lib = os.path.join(REPO, "cs184-raytracer_amd", "rtamd")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
+                    os.path.join(REPO, "tests", "native", "desc_check.cpp"), "-L" + lib, "-lrtamd",
+                    "-Wl,-rpath," + lib], check=True)
+    p = subprocess.run([str(exe), str(tmp_path), "render"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    got = np.fromfile(tmp_path / "desc.raw", dtype=np.float64).reshape(90, 160, 3)
+    want, _ = oracle.render(str(tmp_path / "scene.rti"), 160, 90, bdepth=5)
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
+@pytest.mark.parametrize("scene,bdepth,io", [("excess_inputs/bunny.rti", 4, False), ("inputs/input-09.rti", 10, False),
+                                             ("inputs/input-02.rti", 0, True)])
+def test_render_rgb8_host(gpu, scene, bdepth, io):
+    """rt_render_rgb8 == convertToRGBImage(rt_render) (writers.cpp:4-9), --intersection-only
+    normalised by the global maximum first (scene.cpp:50-58)."""
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    o = gpu.Options(renderWidth_=83, renderHeight_=47, bounceDepth_=bdepth, intersectionOnly_=io)
+    img = s.renderScene(options=o)
+    rgb = s.render_rgb8(options=o)
+    assert np.array_equal(rgb, gpu.to_rgb8(img))
+    if not io:
+        part = s.render_rgb8(options=o, rows=(1, 47, 3))
+        assert np.array_equal(part, rgb[1::3])
+    s.close()
+
+
+def test_intersection_only_rgb8_device_output(gpu):
+    """rt_render_device with --intersection-only and only an RGB8 output: normalised from a
+    staging f64 image (it used to return without writing the bytes)."""
+    torch = pytest.importorskip("torch")
+    scene = "inputs/input-03.rti"
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    o = gpu.Options(renderWidth_=64, renderHeight_=40, intersectionOnly_=True)
+    img = s.renderScene(options=o)
+    out8 = torch.zeros((40, 64, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    s.render_device(s.params(64, 40, 10, True), 0, out8.data_ptr())
+    assert np.array_equal(out8.cpu().numpy(), gpu.to_rgb8(img))
+    with pytest.raises(gpu.ArgumentError):
+        s.render_device(s.params(64, 40, 10, True, 0, 40, 2), 0, out8.data_ptr())
+    s.close()
+
+
+def test_progress_is_incremental_and_complete(gpu):
+    """Progress from the calling thread: starts at 0, never decreases, ends at the total."""
+    scene = "excess_inputs/refraction3.rti"
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    calls = []
+    o = gpu.Options(renderWidth_=512, renderHeight_=512, bounceDepth_=8)
+    img = s.renderScene(options=o, phandler=lambda c, t: calls.append((c, t)), chunk_pixels=16384)
+    total = 512 * 512
+    assert calls[0] == (0, total) and calls[-1] == (total, total)
+    assert all(t == total for _, t in calls)
+    assert all(a[0] <= b[0] for a, b in zip(calls, calls[1:]))
+    rgb = s.render_rgb8(options=o, phandler=lambda c, t: calls.append((c, t)))
+    assert np.array_equal(rgb, gpu.to_rgb8(img))
+    s.close()
+
+
+def test_many_lights(gpu, oracle, tmp_path):
+    """70 point lights (+ ambient): more than the fused shading's 64-bit verdict mask; the
+    light-major layout and k_shade take them (scene.cpp:77-108 loops over any number)."""
+    lines = ["cam 0 0 6  -1.6 -0.9 2  1.6 -0.9 2  -1.6 0.9 2  1.6 0.9 2"]
+    rng = np.random.default_rng(5)
+    for k in range(70):
+        x, y, z = rng.uniform(-6, 6, 3)
+        lines.append(f"ltp {x:.6f} {y:.6f} {z + 6:.6f}  {0.01 * (k % 7):.3f} 0.012 0.015")
+    lines += ["lta 0.1 0.1 0.1", "mat 0.1 0.1 0.1 0.5 0.5 0.5 0.4 0.4 0.4 8 0.3 0.3 0.3",
+              "sph 0 0 0 1", "sph 1.5 0.3 -1 0.6",
+              "xft 0.17 -1.1 0", "xfs 10 10 10", f'obj "{os.path.join(SCENES, "excess_inputs", "bunny.obj")}"', "xfz",
+              "tri -10 -1.2 10  10 -1.2 10  10 -1.2 -10"]
+    f = tmp_path / "lights70.rti"
+    f.write_text("\n".join(lines) + "\n")
+    want, cnt = oracle.render(str(f), 64, 40, bdepth=3)
+    s = gpu.load_scene(str(f))
+    img = s.renderScene(options=gpu.Options(renderWidth_=64, renderHeight_=40, bounceDepth_=3))
+    assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
+    assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+    s.close()
+
+
+@pytest.mark.parametrize("after", [0, 1, 3])
+def test_render_after_a_failed_render_is_exact(gpu, oracle, after):
+    """A device failure in the middle of a render (injected after `after` closest-hit
+    launches) returns an error; the scene's next render is complete, bit-exact and counts
+    exactly its own rays (no stale lane, counter or error word)."""
+    scene = "excess_inputs/bunny.rti"
+    w, h, bdepth = 80, 45, 4
+    want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth)
+    s.renderScene(options=o)  # lanes and level buffers exist
+    s.debug_fail_after(after)
+    with pytest.raises(gpu.DeviceError, match="injected"):
+        s.renderScene(options=o)
+    img = s.renderScene(options=o)
+    assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
+    assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+    s.close()
+
+
+@pytest.mark.parametrize("fuse", ["0", "1"])
+@pytest.mark.parametrize("scene", ["excess_inputs/bunny.rti", "inputs/input-06.rti"])
+def test_fused_multi_level_shadow_batches(gpu, oracle, scene, fuse, monkeypatch):
+    """All-lights shadow layout for the deep levels too (SHADOW_ALL_LIGHTS 3), packets for
+    every level (PACKET_MASK 63) and one direct level, so deep levels are shaded in
+    multi-level batches with and without the fused Phong terms."""
+    w, h, bdepth = 72, 40, 6
+    want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
+    for k, v in (("RTAMD_SHADOW_ALL_LIGHTS", "3"), ("RTAMD_PACKET_MASK", "63"), ("RTAMD_DIRECT_LEVELS", "1"),
+                 ("RTAMD_FUSE_SHADE", fuse)):
+        monkeypatch.setenv(k, v)
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    img = s.renderScene(options=gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth))
+    assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
+    assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+    s.close()
+
+
+def test_camera_eye_direction_vector_raises(gpu):
+    """A camera eye with w == 0 (only possible through the descriptor) throws the Ray
+    origin check's MathException (rtbase.h:13-14)."""
+    src = gpu.load_scene(os.path.join(SCENES, "inputs/input-01.rti"))
+    d = src.desc()
+    d.camera.eye[3] = 0.0
+    s = gpu.Scene.from_desc(d)
+    with pytest.raises(gpu.MathException, match="ray origin is a direction vector"):
+        s.renderScene(options=gpu.Options(renderWidth_=8, renderHeight_=8))
+    s.close()
+    src.close()
