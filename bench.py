@@ -3,37 +3,53 @@
 
 Workload (BASELINE.json configs[2], the metric's 1920x1080 single-GPU config):
 excess_inputs/bunny.rti (4,968-triangle bunny + reflective floor +
-mirror spheres), 1920x1080, --bdepth 4.  A step renders frames of that scene through
-the C-ABI (librtamd.so); rays = traceRay calls (primary + reflection + refraction) +
-shadow rays, counted by the kernels and equal to the reference's counts.
+mirror spheres), 1920x1080, --bdepth 4.  A step renders a fixed batch of frames
+(--frames-per-step, default 8) of that scene through the C-ABI (librtamd.so); rays =
+traceRay calls (primary + reflection + refraction) + shadow rays, counted by the kernels
+and equal to the reference's counts.  Inputs (the scene) are resident in HBM before the
+timed region; every frame is written as the reference's f64 RasterImage and as RGB8.
 
-Multi-GPU (torchrun, one rank per GPU, RCCL): a step renders a batch of N frames, each
-row-interleaved over all N ranks and assembled on rank 0 by an RCCL gather of its RGB8
-rows over xGMI (rtamd.dist.gather_batch).  The interleave rotates with the frame (frame
-f's rows of residue k are rendered by rank (k - f) mod N), so each rank renders every row
-once per step in ONE render call: per-GPU work is one frame per step (weak scaling) and
-each GPU pays the per-call latency of the level chain once per step, not once per frame.
+Multi-GPU (torchrun, one rank per GPU, RCCL over xGMI), --mode partition (default): every
+frame is row-partitioned over the N ranks (row r -> rank r mod N, the reference's
+image-space decomposition of scene.cpp:13-48 spread over GPUs), each rank renders its rows
+of all frames of the step (pipelined, rt_render_batch_device) and every frame's RGB8 rows
+are gathered to rank 0 over RCCL.  The total work per step is fixed: "scaling": "strong".
+--mode replica: frame-parallel instead (each rank renders whole frames, gathered to rank 0;
+weak scaling).
+
+In the same run (rank 0 prints ONE JSON line):
+  - strong_scaling: ONE frame of each --sweep config (default C5 refraction3 4096^2 depth 8
+    and C4 airboat 1920x1080, the 8-GPU configs) row-partitioned over n = 1, 2, 4, 8 <= N
+    ranks (sub-communicators), gathered over RCCL: ms, speed-up, per-rank render ms and the
+    imbalance (max / mean);
+  - roofline of the dominant kernel on a non-overlapping time base: a solo pass
+    (RTAMD_SERIAL=1: every kernel alone on one stream, HIP events around each launch)
+    against the L2 (algorithmic bytes), HBM (PMC-measured bytes, profiles/) and FP64 roofs;
+  - cpu_baseline: the unmodified reference (oracle/_ref) on this host's cores.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3_bunny_1920x1080_bd4]
 """
 import argparse
+import glob
 import json
 import os
+import statistics
 import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "cs184-raytracer_amd"))
-sys.path.insert(0, os.path.join(REPO, "tests"))
 
-HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md, memory hierarchy)
+L2_PEAK_GBS = 34500.0       # MI355X aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md, L2)
+FP64_PEAK_TFLOPS = 78.6     # MI355X vector FP64 (SURVEY.md §8d)
 NODE_BYTES, TRI_BYTES, NRM_BYTES = 64, 72, 72   # SURVEY.md §8d algorithmic bytes (64-B fp32-box node)
 RAY_IO_BYTES, PIXEL_BYTES = 64 + 64, 24
-FP64_PEAK_TFLOPS = 78.6     # MI355X vector FP64 (SURVEY.md §8d)
 # algorithmic fp64 flops (SURVEY.md §8d): node visit = two 28-flop slab tests; a triangle
 # test 38 flops to the a-reject, +67 for one that reaches the normal + facing test; a
 # sphere test 30 + two 28-flop transforms + 12 for the re-normalisation
 NODE_FLOPS, TRI_FLOPS, CAND_FLOPS, SPHERE_FLOPS = 56, 38, 67, 98
+STAGES = ["k_closest", "k_shadow", "k_shade"]
 
 
 def parse():
@@ -44,15 +60,36 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C3_bunny_1920x1080_bd4")
-    ap.add_argument("--frames-per-gpu", type=int, default=4,
-                    help="frames per GPU per step, pipelined over the scene's lanes (rt_render_batch_device)")
+    ap.add_argument("--mode", default="partition", choices=["partition", "replica"])
+    ap.add_argument("--emulate-ranks", type=int, default=1,
+                    help="development: on ONE GPU, render only rank 0's rows of an N-way partition (the per-GPU "
+                         "work of an N-GPU run, to tune it without N GPUs); the line then reports that share")
+    ap.add_argument("--frames-per-step", type=int, default=16,
+                    help="frames per step (partition: in total, every frame split over the ranks; "
+                         "replica: per rank)")
+    ap.add_argument("--sweep", default="C5_refraction3_4096_bd8,C4_airboat_sub_1920x1080",
+                    help="configs whose single frame is row-partitioned over 1, 2, 4, 8 ranks ('' = none)")
+    ap.add_argument("--sweep-reps", type=int, default=3)
+    ap.add_argument("--solo-frames", type=int, default=3,
+                    help="frames rendered with every kernel alone (RTAMD_SERIAL=1) for the roofline time base")
+    ap.add_argument("--solo-only", action="store_true",
+                    help="run only the solo pass (the command rocprofv3 profiles for the roofline)")
     ap.add_argument("--latency-frames", type=int, default=5,
                     help="single-frame renders timed after the run (wall-clock latency of one frame)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic_round1.json"),
-                    help="PMC-measured HBM bytes per trace launch (rocprofv3 FETCH_SIZE/WRITE_SIZE), if present")
+    ap.add_argument("--traffic", default=None,
+                    help="PMC-measured HBM bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE); default: the "
+                         "latest profiles/round*/traffic.json")
     return ap.parse_args()
+
+
+def latest_traffic():
+    cands = sorted(glob.glob(os.path.join(REPO, "profiles", "round*", "traffic.json")))
+    if cands:
+        return cands[-1]
+    old = os.path.join(REPO, "profiles", "traffic_round1.json")
+    return old if os.path.exists(old) else None
 
 
 def _cores():
@@ -68,7 +105,7 @@ def cpu_baseline(s, scene, w, h, bdepth, target_s):
 
     Prefers the UNMODIFIED reference (oracle/_ref/refharness, built from /root/reference/src
     by `make -C oracle ref`; its fork-parallel pixel loop = one reference process per core);
-    falls back to the bit-exact CPU restatement oracle/ (\"port\").  Rays in the sample are
+    falls back to the bit-exact CPU restatement oracle/ ("port").  Rays in the sample are
     the kernels' counts for the same rows (equal to the reference's, see tests)."""
     import subprocess
     import rtamd
@@ -124,6 +161,178 @@ def same_algorithm_baseline(scene, w, h, bdepth, target_s):
                       f"zero-term decisions), {runs} whole {w}x{h} frames: {rays} rays in {secs:.1f} s of render time"}
 
 
+def stage_work(st):
+    """SURVEY.md §8d algorithmic bytes and flops per kernel family of one render's counters."""
+    nbytes, flops = [0, 0, 0], [0, 0, 0]
+    for k, nrays in ((0, st.trace_rays), (1, st.shadow_rays)):
+        nbytes[k] = (nrays * RAY_IO_BYTES + st.stage_node_visits[k] * NODE_BYTES + st.stage_tri_tests[k] * TRI_BYTES +
+                     st.stage_candidates[k] * NRM_BYTES)
+        flops[k] = (st.stage_node_visits[k] * NODE_FLOPS + st.stage_tri_tests[k] * TRI_FLOPS +
+                    st.stage_candidates[k] * CAND_FLOPS + st.stage_sphere_tests[k] * SPHERE_FLOPS)
+    nbytes[2] = st.pixels * PIXEL_BYTES
+    return nbytes, flops
+
+
+def solo_pass(scene_path, W, H, kw, frames, device):
+    """Every kernel alone: a scene created with RTAMD_SERIAL=1 runs the shading kernels on the
+    closest-hit chain's stream, so the HIP events around each launch bracket that kernel and
+    nothing else (the throughput schedule overlaps levels and frames)."""
+    import rtamd
+    import torch
+    old = os.environ.get("RTAMD_SERIAL")
+    os.environ["RTAMD_SERIAL"] = "1"
+    try:
+        s = rtamd.load_scene(scene_path, device=device)
+        s.upload()
+    finally:
+        if old is None:
+            del os.environ["RTAMD_SERIAL"]
+        else:
+            os.environ["RTAMD_SERIAL"] = old
+    out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
+    out8 = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)
+    stream = torch.cuda.current_stream().cuda_stream
+    s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)  # allocations
+    acc = {"ms": [0.0] * 3, "launches": [0] * 3, "bytes": [0] * 3, "flops": [0] * 3, "wall": 0.0}
+    for _ in range(frames):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)
+        acc["wall"] += time.perf_counter() - t0
+        nb, fl = stage_work(st)
+        for k in range(3):
+            acc["ms"][k] += st.stage_ms[k]
+            acc["launches"][k] += st.stage_launches[k]
+            acc["bytes"][k] += nb[k]
+            acc["flops"][k] += fl[k]
+    s.close()
+    return acc
+
+
+def roofline(solo, frames, traffic_path, concurrent):
+    """Dominant kernel (largest solo time per frame) against three roofs; `bound` = the roof
+    it is closest to.  achieved / peak / frac are that roof's; every fraction is listed."""
+    dom = max(range(3), key=lambda k: solo["ms"][k])
+    name = STAGES[dom]
+    launches = solo["launches"][dom]
+    t_launch_s = solo["ms"][dom] / launches * 1e-3
+    alg_bytes = solo["bytes"][dom] / launches
+    flops = solo["flops"][dom] / launches
+    traffic, traffic_note = None, None
+    if traffic_path and os.path.exists(traffic_path):
+        try:
+            tj = json.load(open(traffic_path))
+            traffic = tj.get("hbm_bytes_per_launch", {}).get(name)
+            traffic_note = os.path.relpath(traffic_path, REPO) + ": " + tj.get("method", "")
+        except (OSError, ValueError):
+            traffic = None
+    roofs = {
+        "l2": {"achieved": alg_bytes / t_launch_s / 1e9, "peak": L2_PEAK_GBS, "unit": "GB/s",
+               "what": "SURVEY.md §8d algorithmic bytes (ray I/O + LBVH nodes + triangles + normals; the scene "
+                       "is L2/MALL-resident) / solo launch time vs the aggregate L2 bandwidth"},
+        "fp64": {"achieved": flops / t_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "what": "SURVEY.md §8d algorithmic FP64 flops / solo launch time vs vector FP64 peak"},
+    }
+    if traffic:
+        roofs["hbm"] = {"achieved": traffic / t_launch_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "what": "PMC HBM bytes per launch (FETCH_SIZE, WRITE_SIZE; profiles/) / solo launch time"}
+    for r in roofs.values():
+        r["frac"] = r["achieved"] / r["peak"]
+        r["achieved"] = round(r["achieved"], 3)
+        r["frac"] = round(r["frac"], 4)
+    bound = max(roofs, key=lambda k: roofs[k]["frac"])
+    b = roofs[bound]
+    return {
+        "bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"], "frac": b["frac"],
+        "traffic": traffic, "kernel": name,
+        "time_base": f"solo: {frames} frames with RTAMD_SERIAL=1 (every kernel alone on one stream), HIP events "
+                     "around each launch on that stream; rocprofv3 of `bench.py --solo-only` gives the same "
+                     "durations (profiles/)",
+        "avg_launch_ms": round(t_launch_s * 1e3, 4), "launches_per_frame": launches / frames,
+        "algorithmic_bytes_per_launch": round(alg_bytes), "fp64_flops_per_launch": round(flops),
+        "hbm_algorithmic": {"achieved": round(alg_bytes / t_launch_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(alg_bytes / t_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                            "note": "the contract's reading (algorithmic bytes vs HBM); the scene reads are "
+                                    "served on die, so `hbm` (PMC bytes) is the HBM figure"},
+        "roofs": roofs, "traffic_source": traffic_note,
+        "solo_ms_per_frame": {STAGES[k]: round(solo["ms"][k] / frames, 4) for k in range(3)},
+        "solo_frame_wall_ms": round(solo["wall"] / frames * 1e3, 3),
+        "concurrent": concurrent,
+    }
+
+
+def strong_scaling(a, world, rank, local, groups, dist, torch):
+    """ONE frame of each sweep config, row-interleaved over n = 1, 2, 4, 8 <= world ranks and
+    gathered to rank 0 over RCCL (RGB8), timed end to end; ranks >= n idle."""
+    import rtamd
+    from rtamd import dist as rd
+    from rtamd.configs import CONFIGS, SCENES, option_kwargs
+    out = {}
+    for cfg in [c for c in a.sweep.split(",") if c]:
+        scene_rel, W, H, flags = CONFIGS[cfg]
+        kw = option_kwargs(flags)
+        s = rtamd.load_scene(os.path.join(SCENES, scene_rel), device=local)
+        s.upload()
+        stream = torch.cuda.current_stream().cuda_stream
+        rows_curve = []
+        for n, grp in groups:
+            n_max = -(-H // n)
+            buf = torch.zeros((n_max, W, 3), dtype=torch.uint8, device="cuda")
+            frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+            bufs = [torch.empty_like(buf) for _ in range(n)] if rank == 0 and n > 1 else None
+            prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rank, H, n) if rank < n else None
+            samples = []
+            for rep in range(a.sweep_reps + 1):  # rep 0: warm-up (level buffers for this row count)
+                if world > 1:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                rays, t_render = 0, 0.0
+                if rank < n:
+                    st = s.render_device(prm, 0, buf.data_ptr(), stream)
+                    torch.cuda.synchronize()
+                    t_render = time.perf_counter() - t0
+                    rays = st.rays
+                    if n > 1:
+                        rd.gather_rows(buf, H, dst=0, out=frame, bufs=bufs, group=grp, group_size=n, group_rank=rank)
+                    elif rank == 0:
+                        frame.copy_(buf)
+                    torch.cuda.synchronize()
+                t_total = time.perf_counter() - t0
+                v = torch.tensor([t_render, t_total, float(rays)], dtype=torch.float64, device="cuda")
+                if world > 1:
+                    allv = [torch.empty_like(v) for _ in range(world)]
+                    dist.all_gather(allv, v)
+                    allv = [x.tolist() for x in allv[:n]]
+                else:
+                    allv = [v.tolist()]
+                if rep > 0:
+                    samples.append(allv)
+            if rank == 0:
+                tot = [max(r[1] for r in smp) for smp in samples]
+                med = statistics.median_low(tot)
+                pick = samples[tot.index(med)]
+                rend = [r[0] * 1e3 for r in pick]
+                rays = sum(r[2] for r in pick)
+                rows_curve.append({"n_gpus": n, "ms": round(med * 1e3, 3), "mrays_per_s": round(rays / med / 1e6, 1),
+                                   "render_ms_per_rank": [round(x, 3) for x in rend],
+                                   "imbalance": round(max(rend) / (sum(rend) / len(rend)), 3),
+                                   "gather_ms": round((med - max(r[0] for r in pick)) * 1e3, 3), "rays": int(rays)})
+        if rank == 0:
+            base = rows_curve[0]["ms"]
+            for r in rows_curve:
+                r["speedup"] = round(base / r["ms"], 3)
+                r["efficiency"] = round(base / r["ms"] / r["n_gpus"], 3)
+            out[cfg] = {"scene": scene_rel, "width": W, "height": H, "bounce_depth": kw["bdepth"],
+                        "partition": "rows interleaved (row r -> rank r mod n), RGB8 rows gathered to rank 0 over "
+                                     + ("RCCL" if dist.is_initialized() and dist.get_backend() == "nccl" else
+                                        "the process group" if world > 1 else "(no exchange at n = 1)"),
+                        "curve": rows_curve}
+        s.close()
+    return out
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -132,7 +341,8 @@ def main():
     import torch
     import torch.distributed as dist
     import rtamd
-    from cases import CONFIGS, SCENES, option_kwargs
+    from rtamd import dist as rd
+    from rtamd.configs import CONFIGS, SCENES, option_kwargs
 
     if a.backend == "gloo":
         local = local % torch.cuda.device_count()  # rehearsal: several ranks may share a GPU
@@ -145,63 +355,79 @@ def main():
     scene_rel, W, H, flags = CONFIGS[a.config]
     kw = option_kwargs(flags)
     scene = os.path.join(SCENES, scene_rel)
+    traffic_path = a.traffic or latest_traffic()
+
+    if a.solo_only:  # the profiled command of the roofline's time base
+        solo = solo_pass(scene, W, H, kw, a.solo_frames, local)
+        if rank == 0:
+            print(json.dumps({"solo_only": True, "config": a.config,
+                              "roofline": roofline(solo, a.solo_frames, traffic_path, None)}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     s = rtamd.load_scene(scene, device=local)
     s.upload()
-    n_max = -(-H // world)
-    F = max(1, a.frames_per_gpu)
-    outs = [torch.empty((H, W, 3), dtype=torch.float64, device="cuda") for _ in range(F)]
-    # RGB8 output double-buffered: the gathers of step i (side stream) overlap the render of i+1
-    out8s = [[torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(F)] for _ in range(2)]
+    B = max(1, a.frames_per_step)
+    partition = a.mode == "partition"
+    # this rank's rows of every frame (partition) or whole frames (replica)
+    ways = world if a.emulate_ranks <= 1 else a.emulate_ranks * world
+    rows = rd.rank_rows(H, rank, ways) if partition else (0, H, 1)
+    n_loc = len(range(*rows))
+    n_buf = -(-H // ways) if partition else H  # gather buffers: the longest rank's row count
+    outs = [torch.empty((n_buf, W, 3), dtype=torch.float64, device="cuda") for _ in range(B)]
+    # RGB8 double-buffered: the gathers of step i (side stream) overlap the render of step i+1
+    out8s = [[torch.zeros((n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(B)] for _ in range(2)]
     gathered = [None, None]
     comm = torch.cuda.Stream() if world > 1 else torch.cuda.current_stream()
-    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)  # every row, once per step
+    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], *rows)
     stream = torch.cuda.current_stream().cuda_stream
-    gather = [torch.empty((n_max, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
+    gbufs = [torch.empty((n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
         if rank == 0 and world > 1 else None
-    frames = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] if rank == 0 else None
-    from rtamd import dist as rd
+    n_frames_rank0 = B if partition else B * world
+    frames = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(n_frames_rank0)] \
+        if rank == 0 else None
 
-    totals = {"rays": 0, "trace_rays": 0, "zero": 0, "ms": [0.0, 0.0, 0.0], "launches": [0, 0, 0], "bytes": [0, 0, 0],
-              "flops": [0, 0, 0]}
+    totals = {"rays": 0, "trace_rays": 0, "zero": 0, "ms": [0.0] * 3, "launches": [0] * 3, "bytes": [0] * 3,
+              "flops": [0] * 3}
     work = {}
-
     n_steps = [0]
 
     def step(record):
-        # F x N frames per step (weak scaling): F renders of every row on this rank, pipelined
-        # in one batch call; each render holds this rank's rows of N row-interleaved frames,
-        # assembled on rank 0 by one RCCL gather of RGB8 rows per frame, on a side stream
         k = n_steps[0] % 2
         n_steps[0] += 1
         if gathered[k] is not None:  # the gathers that read these buffers two steps ago
             torch.cuda.current_stream().wait_event(gathered[k])
-        st = s.render_batch_device([prm] * F, [o.data_ptr() for o in outs], [o.data_ptr() for o in out8s[k]],
+        st = s.render_batch_device([prm] * B, [o.data_ptr() for o in outs], [o.data_ptr() for o in out8s[k]],
                                    stream)
         rendered = torch.cuda.Event()
         rendered.record()
         with torch.cuda.stream(comm):
             comm.wait_event(rendered)
-            for f in range(F):
-                rd.gather_batch(out8s[k][f], H, dst=0, frames=frames, bufs=gather)
+            for f in range(B):
+                if partition and ways != world:  # emulated share: no assembly
+                    pass
+                elif partition:  # frame f assembled on rank 0 from every rank's rows
+                    rd.gather_rows(out8s[k][f], H, dst=0, out=frames[f] if rank == 0 else None, bufs=gbufs)
+                elif world > 1:  # whole frames of every rank to rank 0
+                    rd.gather_frames(out8s[k][f], dst=0, out=frames[f * world:(f + 1) * world] if rank == 0 else None)
+                else:
+                    frames[f].copy_(out8s[k][f])
             gathered[k] = torch.cuda.Event()
             gathered[k].record(comm)
         if record:
             totals["rays"] += st.trace_rays + st.shadow_rays
             totals["trace_rays"] += st.trace_rays
             totals["zero"] += st.shadow_rays_zero_terms
-            for k in range(3):
-                totals["ms"][k] += st.stage_ms[k]
-                totals["launches"][k] += st.stage_launches[k]
-            # SURVEY.md §8d algorithmic bytes, attributed to the kernel that moves them
-            for k, nrays in ((0, st.trace_rays), (1, st.shadow_rays)):
-                totals["bytes"][k] += (nrays * RAY_IO_BYTES + st.stage_node_visits[k] * NODE_BYTES +
-                                       st.stage_tri_tests[k] * TRI_BYTES + st.stage_candidates[k] * NRM_BYTES)
-                totals["flops"][k] += (st.stage_node_visits[k] * NODE_FLOPS + st.stage_tri_tests[k] * TRI_FLOPS +
-                                       st.stage_candidates[k] * CAND_FLOPS + st.stage_sphere_tests[k] * SPHERE_FLOPS)
-            totals["bytes"][2] += st.pixels * PIXEL_BYTES
-            per = lambda xs: [x // F for x in xs]  # the batch's F renders do identical work
-            work.update({"trace_rays": st.trace_rays // F, "shadow_rays": st.shadow_rays // F,
-                         "shadow_rays_zero_terms": st.shadow_rays_zero_terms // F,
+            nb, fl = stage_work(st)
+            for j in range(3):
+                totals["ms"][j] += st.stage_ms[j]
+                totals["launches"][j] += st.stage_launches[j]
+                totals["bytes"][j] += nb[j]
+                totals["flops"][j] += fl[j]
+            per = lambda xs: [x // B for x in xs]  # the batch's B renders do identical work
+            work.update({"trace_rays": st.trace_rays // B, "shadow_rays": st.shadow_rays // B,
+                         "shadow_rays_zero_terms": st.shadow_rays_zero_terms // B,
                          "node_visits": per(st.stage_node_visits), "tri_tests": per(st.stage_tri_tests),
                          "candidates": per(st.stage_candidates), "sphere_tests": per(st.stage_sphere_tests),
                          "bvh_traversals": per(st.stage_bvh_traversals),
@@ -216,10 +442,11 @@ def main():
     for _ in range(a.steps):
         step(True)
     torch.cuda.synchronize()
+    t_rank = time.perf_counter() - t0  # this rank's own work done (before waiting for the others)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # wall-clock of ONE frame (this rank's rows, one render call, nothing else in flight)
+    # wall-clock of ONE frame's rows on this rank (one render call, nothing else in flight)
     lat = []
     for _ in range(max(0, a.latency_frames)):
         torch.cuda.synchronize()
@@ -228,37 +455,48 @@ def main():
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t1)
     lat = sorted(lat)[len(lat) // 2] if lat else float("nan")
-    agg = torch.tensor([elapsed, float(totals["rays"])] + totals["ms"] + [float(x) for x in totals["launches"]] +
-                       [float(x) for x in totals["bytes"]] + [float(x) for x in totals["flops"]] +
-                       [float(totals["trace_rays"]), lat, float(totals["zero"])], dtype=torch.float64, device="cuda")
+    vals = [elapsed, float(totals["rays"]), float(totals["trace_rays"]), lat, float(totals["zero"]), t_rank] + \
+        totals["ms"] + [float(x) for x in totals["launches"]] + [float(x) for x in totals["bytes"]] + \
+        [float(x) for x in totals["flops"]]
+    agg = torch.tensor(vals, dtype=torch.float64, device="cuda")
     if world > 1:
-        t_max = agg[0:1].clone()
-        l_max = agg[15:16].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(l_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(agg, op=dist.ReduceOp.SUM)
-        agg[0], agg[15] = t_max[0], l_max[0]
-    v = agg.tolist()
-    elapsed, rays, stage_ms, stage_launches, stage_bytes = v[0], v[1], v[2:5], v[5:8], v[8:11]
-    stage_flops, trace_rays, latency, zero_rays = v[11:14], v[14], v[15], v[16]
-    fps = world * F  # frames per step
+        allv = [torch.empty_like(agg) for _ in range(world)]
+        dist.all_gather(allv, agg)
+        allv = [x.tolist() for x in allv]
+    else:
+        allv = [agg.tolist()]
+    elapsed = max(v[0] for v in allv)  # max over ranks
+    rays = sum(v[1] for v in allv)
+    trace_rays = sum(v[2] for v in allv)
+    latency = max(v[3] for v in allv)
+    zero_rays = sum(v[4] for v in allv)
+    rank_ms = [v[5] / a.steps * 1e3 for v in allv]
+    conc_ms = [sum(v[6 + j] for v in allv) for j in range(3)]
+    conc_launches = [sum(v[9 + j] for v in allv) for j in range(3)]
+    conc_bytes = [sum(v[12 + j] for v in allv) for j in range(3)]
+
+    sweep = {}
+    groups = []
+    n = 1
+    while n <= world:
+        groups.append((n, dist.new_group(list(range(n))) if world > 1 and n > 1 else None))
+        n *= 2
+    if a.sweep:
+        sweep = strong_scaling(a, world, rank, local, groups, dist, torch)
+    solo = solo_pass(scene, W, H, kw, a.solo_frames, local) if rank == 0 and a.solo_frames > 0 else None
+
     if rank == 0:
+        fps = B if partition else B * world  # frames per step
         value = rays / elapsed / 1e6
-        names = ["k_closest", "k_shadow", "k_shade"]
-        dom = max(range(3), key=lambda k: stage_ms[k])  # the dominant kernel
-        kms, launches, nbytes = stage_ms[dom], stage_launches[dom], stage_bytes[dom]
-        achieved = (nbytes / launches) / ((kms / launches) * 1e-3) / 1e9 if launches else 0.0
-        gflops = stage_flops[dom] / (kms * 1e-3) / 1e9 if kms else 0.0
-        traffic = None
-        if os.path.exists(a.traffic):
-            try:
-                traffic = json.load(open(a.traffic)).get("hbm_bytes_per_launch", {}).get(names[dom])
-            except Exception:
-                traffic = None
+        concurrent = {"kernel_ms_per_frame": {STAGES[j]: round(conc_ms[j] / a.steps / fps, 4) for j in range(3)},
+                      "launches_per_frame": {STAGES[j]: conc_launches[j] / a.steps / fps for j in range(3)},
+                      "note": "HIP-event spans of the throughput schedule: launches of different levels and frames "
+                              "overlap, so these spans add up to more than the step; not a time base"}
         res = {
             "metric": "Mrays/s (primary+secondary) and wall-clock at 1920x1080; HBM GB/s vs peak",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong" if partition else "weak",
             "mrays_trace": round(trace_rays / elapsed / 1e6, 3),
             # rays that went through a traversal: the shadow rays decided by zero Phong terms
             #  count in `value` like every other ray the reference casts
@@ -266,27 +504,32 @@ def main():
             "vs_baseline": None, "dtype": "f64", "data": "synthetic: shipped reference scene data (bunny.obj), "
                                                         "deterministic, no RNG",
             "config": {"workload": a.config, "scene": scene_rel, "width": W, "height": H,
-                       "bounce_depth": kw["bdepth"], "frames_per_step": fps, "frames_per_gpu_per_step": F,
+                       "bounce_depth": kw["bdepth"], "frames_per_step": fps,
                        "rays_per_frame": int(rays / a.steps / fps),
                        "ms_per_frame": round(elapsed / a.steps / fps * 1e3, 3),
                        "frame_latency_ms": round(latency * 1e3, 3),
-                       "parallelism": (f"{fps} frames/step: {F} pipelined renders per GPU, each holding its rows of "
-                                       f"{world} frames row-interleaved x{world} (rotated), RCCL gather of RGB8 rows")
-                       if world > 1 else f"1 GPU, {F} frames/step pipelined (rt_render_batch_device)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": names[dom], "avg_launch_ms": round(kms / launches, 4) if launches else None,
-                         "fp64": {"achieved": round(gflops / 1e3, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                  "frac": round(gflops / 1e3 / FP64_PEAK_TFLOPS, 4)},
-                         "note": "algorithmic bytes per SURVEY.md §8d (ray I/O + LBVH nodes + triangles + normals), "
-                                 "mostly L2/MALL-resident scene reads; kernel times are HIP-event spans of launches "
-                                 "that run concurrently with other levels' kernels; see DESIGN.md",
-                         "stages": {names[k]: {"ms_per_frame": round(stage_ms[k] / a.steps / fps, 4),
-                                               "launches_per_frame": stage_launches[k] / a.steps / fps,
-                                               "GBps": round(stage_bytes[k] / (stage_ms[k] * 1e-3) / 1e9, 1)
-                                               if stage_ms[k] else None} for k in range(3)},
-                         "work_per_frame_rank0": work},
+                       "parallelism": (f"EMULATED rank share: rank 0's {n_loc} of {H} rows of an {ways}-way "
+                                       f"partition, {fps} frames/step on 1 GPU (development measure, not a job)"
+                                       if ways != world else
+                                       f"{fps} frames/step, each row-interleaved over {world} GPU(s) "
+                                       f"({n_loc} rows of {H} on rank 0), pipelined renders per GPU, "
+                                       f"{'RCCL' if a.backend == 'nccl' else 'gloo (rehearsal)'} gather "
+                                       "of every frame's RGB8 rows to rank 0" if partition and world > 1 else
+                                       f"1 GPU, {fps} frames/step pipelined (rt_render_batch_device)" if world == 1
+                                       else f"frame-parallel: {B} whole frames per GPU per step, gathered to rank 0")},
+            "per_rank": {"ms_per_step": [round(x, 3) for x in rank_ms],
+                         "imbalance": round(max(rank_ms) / (sum(rank_ms) / len(rank_ms)), 3)},
+            "roofline": roofline(solo, a.solo_frames, traffic_path, concurrent) if solo else None,
+            "work_per_frame_rank0": work,
+            "strong_scaling": sweep,
         }
+        if res["roofline"]:
+            # the dominant kernel's solo time per step must fit in the step (a consistent time base)
+            dom = res["roofline"]["kernel"]
+            res["roofline"]["solo_ms_per_step"] = round(res["roofline"]["solo_ms_per_frame"][dom] * fps / world, 3)
+            res["roofline"]["concurrent"]["algorithmic_GBps_event_spans"] = round(
+                conc_bytes[STAGES.index(dom)] / (conc_ms[STAGES.index(dom)] * 1e-3) / 1e9, 1) \
+                if conc_ms[STAGES.index(dom)] else None
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(s, scene, W, H, kw["bdepth"], a.cpu_seconds)
             same = same_algorithm_baseline(scene, W, H, kw["bdepth"], a.cpu_seconds / 3)
@@ -295,6 +538,7 @@ def main():
         print(json.dumps(res), flush=True)
     s.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -39,6 +39,7 @@ const char* device_error_text(int code) {  // MathException what() (rtbase.h:14-
 		case rtamd::DERR_POINT_DIRECTION: return "ray direction is a point vector";
 		case rtamd::DERR_STACK: return "internal: BVH traversal stack overflow";
 		case rtamd::DERR_ORIGIN_DIRECTION: return "ray origin is a direction vector";
+		case rtamd::DERR_PLAN: return "internal: a replayed launch plan did not fit the render";
 		default: return "unknown device error";
 	}
 }
@@ -81,6 +82,33 @@ struct LevelBuffers {
 	void* block = nullptr;
 };
 
+// A chunk shape traced once host-driven becomes a plan: the same launch sequence with every
+// level size read on the device (k_closest's n from the previous level's child counter,
+// the shading batches and reductions from the hit and child counters), captured once into
+// a hipGraph and replayed for every later chunk of that shape with one hipGraphLaunch.
+// A frame's launches then cost the host one call instead of ~70.  Levels and
+// capacities come from the traced chunk; a replay that would need more (a deeper level, a
+// larger level) is caught on the device (DERR_PLAN, nothing written past a buffer) and the
+// render is redone host-driven.
+struct PlanKey {
+	int32_t width, height, row_begin, row_step, chunk_row0, depth, io;
+	int64_t n0;
+	bool operator==(const PlanKey& o) const {
+		return width == o.width && height == o.height && row_begin == o.row_begin && row_step == o.row_step &&
+		       chunk_row0 == o.chunk_row0 && depth == o.depth && io == o.io && n0 == o.n0;
+	}
+};
+
+struct Plan {
+	PlanKey key{};
+	int n_levels = 0;
+	// rays and hits of every level in the traced chunk: they size the grids only (the kernels
+	// read the actual counts and stride over them, so a difference costs time, not results)
+	std::vector<int64_t> level_n, hits;
+	int launches[3] = {0, 0, 0};
+	hipGraphExec_t exec = nullptr;
+};
+
 // One render pipeline: its own level buffers, streams and events, tracing one chunk of
 // rows (<= 4 M pixels) at a time as a host-polled state machine (Render below).  Several
 // lanes can trace chunks of a frame concurrently (RTAMD_LANES); on C3 one lane is
@@ -113,7 +141,20 @@ struct Lane {
 	std::vector<int64_t> level_n;         // ray counts of the levels known so far
 	std::vector<int> shaded;                        // first level of each shading launch
 	std::vector<std::pair<int, int64_t>> deferred;  // (level, hits) shaded after the chain
+	// launch plans (hipGraphs) of the chunk shapes this lane has traced; invalid once a level
+	// buffer is reallocated
+	std::vector<Plan> plans;
+	const Plan* planned = nullptr;        // the plan replaying the current chunk, if any
+	rtamd::JobIO* jobio_dev = nullptr;    // the chunk's output pointers (read by k_output)
+	rtamd::JobIO* jobio_pin = nullptr;    // pinned staging of jobio_dev (one chunk in flight)
 };
+
+void clear_plans(Lane& ln) {
+	for (Plan& p : ln.plans)
+		if (p.exec) (void)hipGraphExecDestroy(p.exec);
+	ln.plans.clear();
+	ln.planned = nullptr;
+}
 
 struct rt_scene {
 	int device = 0;
@@ -139,6 +180,11 @@ struct rt_scene {
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
 	int fuse_shade = 1;                          // RTAMD_FUSE_SHADE: all-lights k_shadow levels shade in place
+	// RTAMD_GRAPH: launch plans of traced chunk shapes: 0 off (every chunk host-driven), 1
+	// replayed as hipGraphs, 2 issued directly (default: this ROCm's graph replay serialises
+	// the branches and the lanes)
+	int graphs = 2;
+	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
 	int shadow_all_lights = 1;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// measured best on C3: packets for the camera rays and their first bounce, and
 	// for the shadow rays of both (once the zero-term decision thinned the per-lane waves)
@@ -167,6 +213,7 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	if (ln.levels.size() <= level) ln.levels.resize(level + 1);
 	LevelBuffers& L = ln.levels[level];
 	if (L.lv.capacity >= capacity) return RT_OK;
+	clear_plans(ln);  // the plans' graphs hold this lane's buffer pointers
 	if (L.block) {
 		HIP_TRY(hipDeviceSynchronize());
 		HIP_TRY(hipFree(L.block));
@@ -198,7 +245,7 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	L.lv.hinside = reinterpret_cast<uint8_t*>(take(n));
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
-	HIP_TRY(hipMemset(L.lv.counts, 0, 2 * sizeof(int32_t)));
+	HIP_TRY(hipMemset(L.lv.counts, 0, 4 * sizeof(int32_t)));
 	L.lv.capacity = capacity;
 	return RT_OK;
 }
@@ -207,6 +254,7 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 // earlier level never changes while copies of it may be in flight).
 int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	if (level + 1 > ln.levels_cap) {
+		clear_plans(ln);
 		HIP_TRY(hipDeviceSynchronize());
 		const size_t cap = std::max<size_t>(16, 2 * (level + 1));
 		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
@@ -254,10 +302,15 @@ int lane_create(Lane& ln, int prio_low, int prio_high) {
 	HIP_TRY(hipStreamCreateWithPriority(&ln.readback, hipStreamNonBlocking, prio_high));
 	for (hipStream_t& q : ln.shade) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
 	HIP_TRY(hipEventCreateWithFlags(&ln.chunk_done, hipEventDisableTiming));
+	HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ln.jobio_dev), sizeof(rtamd::JobIO)));
+	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.jobio_pin), sizeof(rtamd::JobIO), hipHostMallocDefault));
 	return RT_OK;
 }
 
 void lane_destroy(Lane& ln) {
+	clear_plans(ln);
+	if (ln.jobio_dev) (void)hipFree(ln.jobio_dev);
+	if (ln.jobio_pin) (void)hipHostFree(ln.jobio_pin);
 	for (auto& L : ln.levels)
 		if (L.block) (void)hipFree(L.block);
 	if (ln.levels_pinned) (void)hipHostFree(ln.levels_pinned);
@@ -344,6 +397,164 @@ struct Render {
 		return RT_OK;
 	}
 
+	PlanKey key_of(const Lane& ln, const Job& job) const {
+		PlanKey k{};
+		k.width = ln.fg.width;
+		k.height = ln.fg.height;
+		k.row_begin = ln.fg.row_begin;
+		k.row_step = ln.fg.row_step;
+		k.chunk_row0 = ln.fg.chunk_row0;
+		k.depth = job.depth;
+		k.io = job.io;
+		k.n0 = ln.n0;
+		return k;
+	}
+
+	Plan* find_plan(Lane& ln, const PlanKey& k) const {
+		if (!s->graphs || s->serial) return nullptr;
+		for (Plan& p : ln.plans)
+			if (p.key == k) return &p;
+		return nullptr;
+	}
+
+	// shading of the levels `lv` with their hit counts read on the device (plans; the grid
+	// from the plan's traced hits)
+	int launch_shading_dev(Lane& ln, const std::vector<int>& lv, hipStream_t q, Plan& pl) {
+		rtamd::ShadeBatch b{};
+		const int64_t nl = s->ds.n_nonambient;
+		auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
+		int64_t so = 0, ho = 0;  // upper bounds (the levels' capacities): grid sizes only
+		b.n = static_cast<int32_t>(lv.size());
+		b.dev_counts = 1;
+		b.all_lights = (s->shadow_all_lights >> (lv.front() == 0 ? 0 : 1)) & 1;
+		for (int k = 0; k < b.n; k++) {
+			const rtamd::RayLevel& L = ln.levels[lv[k]].lv;
+			b.level[k] = lv[k];
+			b.nh_dev[k] = L.counts;
+			so += (b.all_lights ? 1 : nl) * wave_up(pl.hits[lv[k]]);
+			ho += wave_up(pl.hits[lv[k]]);
+		}
+		// grid sizes from the traced chunk's hits (at least one block: the kernels stride)
+		b.shadow_begin[b.n] = std::max<int64_t>(so, 64);
+		b.shade_begin[b.n] = std::max<int64_t>(ho, 64);
+		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(b, s->packet_mask);
+		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
+		if (nl > 0) pl.launches[1]++;
+		if (!b.fused) {
+			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
+			pl.launches[2]++;
+		}
+		return RT_OK;
+	}
+
+	// The launch sequence of a planned chunk with device-read level sizes, issued at once
+	// (no host round trip between levels): the same streams and dependencies as the
+	// host-driven schedule: the chain on ln.stream, direct levels' shading on shade[L % 3]
+	// as soon as their k_closest is done, the deep levels in batches on shade[3] after the
+	// chain, then reductions and the output.  capture: recorded into a graph (the output
+	// pointers then come from ln.jobio_dev), with events of its own.
+	int issue_plan(Lane& ln, const Job& job, Plan& pl, bool capture) {
+		const int nlev = pl.n_levels, depth = job.depth;
+		int rc = RT_OK;
+		std::vector<hipEvent_t> tmp;
+		if (!capture && (rc = ensure_events(ln, nlev))) return rc;
+		// event slots as in the host-driven schedule: [L][1] k_closest(L) done, [L][4] the
+		// shading launch starting at level L done
+		auto ev = [&](int L, int k) -> hipEvent_t {
+			if (!capture) return ln.level_events[L][k];
+			hipEvent_t e = nullptr;
+			if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+			tmp.push_back(e);
+			return e;
+		};
+		auto step = [&](hipError_t e) {
+			if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string("planned launch: ") + hipGetErrorString(e));
+		};
+		int launches[3] = {0, 0, 0};
+		const int64_t W = job.W;
+		double* out = capture || !job.out_rgb_dev ? nullptr : job.out_rgb_dev + ln.r0 * W * 3;
+		uint8_t* out8 = capture || !job.out_rgb8_dev ? nullptr : job.out_rgb8_dev + ln.r0 * W * 3;
+		hipStream_t st = ln.stream;
+		std::vector<hipEvent_t> joins;
+		Plan scratch = pl;
+		for (int L = 0; L < nlev && rc == RT_OK; L++) {
+			const int remaining = depth - L;
+			const bool last = L == nlev - 1;
+			const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
+			step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
+			                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
+			                           last && remaining > 0));
+			launches[0]++;
+			hipEvent_t done = ev(L, 1);
+			step(done ? hipEventRecord(done, st) : hipErrorOutOfMemory);
+			// shading beside the chain only where a later level's tracing can overlap it: a
+			// wait on a not yet signalled event of another queue costs tens of microseconds
+			if (L < s->direct_levels && rc == RT_OK) {
+				const bool side = L < nlev - 1;
+				hipStream_t q = side ? ln.shade[L % 3] : st;
+				if (side) step(hipStreamWaitEvent(q, done, 0));
+				scratch.launches[1] = scratch.launches[2] = 0;
+				if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch);
+				launches[1] += scratch.launches[1];
+				launches[2] += scratch.launches[2];
+				if (side) {
+					hipEvent_t sh = ev(L, 4);
+					step(sh ? hipEventRecord(sh, q) : hipErrorOutOfMemory);
+					joins.push_back(sh);
+				}
+			}
+		}
+		// the deep levels after the chain, on its own stream (the reductions wait for them)
+		if (rc == RT_OK && nlev > s->direct_levels) {
+			hipStream_t q = st;
+			std::vector<int> deep;
+			for (int L = s->direct_levels; L < nlev; L++) deep.push_back(L);
+			for (size_t k = 0; k < deep.size() && rc == RT_OK; k += rtamd::kMaxBatch) {
+				const size_t e = std::min(deep.size(), k + rtamd::kMaxBatch);
+				scratch.launches[1] = scratch.launches[2] = 0;
+				rc = launch_shading_dev(ln, std::vector<int>(deep.begin() + k, deep.begin() + e), q, scratch);
+				launches[1] += scratch.launches[1];
+				launches[2] += scratch.launches[2];
+			}
+		}
+		for (hipEvent_t j : joins)
+			if (rc == RT_OK) step(hipStreamWaitEvent(st, j, 0));
+		for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
+			step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1, ln.levels[l].lv,
+			                                ln.levels[l + 1].lv, st));
+		if (rc == RT_OK)
+			step(rtamd::launch_output(ln.n0, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, out, out8,
+			                          capture ? ln.jobio_dev : nullptr, job.io, s->stats, st));
+		for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
+		for (hipEvent_t e : tmp) (void)hipEventDestroy(e);
+		return rc;
+	}
+
+	// A plan for the chunk just traced host-driven (its shape: ln.fg, ln.n0, the job's
+	// depth; its levels: ln.level_n); with RTAMD_GRAPH=1 also captured into a hipGraph.
+	int build_plan(Lane& ln, const Job& job) {
+		Plan pl;
+		pl.key = key_of(ln, job);
+		pl.n_levels = static_cast<int>(ln.level_n.size());
+		pl.level_n = ln.level_n;
+		for (int L = 0; L < pl.n_levels; L++) pl.hits.push_back(ln.counts_host[2 * L]);
+		if (s->plan_truncate && pl.n_levels > 1) pl.n_levels--;  // test hook: a plan that must miss
+		if (s->graphs == 1) {
+			hipGraph_t graph = nullptr;
+			HIP_TRY(hipStreamBeginCapture(ln.stream, hipStreamCaptureModeThreadLocal));
+			int rc = issue_plan(ln, job, pl, true);
+			const hipError_t ec = hipStreamEndCapture(ln.stream, &graph);
+			if (rc == RT_OK && ec != hipSuccess)
+				rc = fail(RT_ERR_DEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
+			if (rc == RT_OK && hipGraphInstantiate(&pl.exec, graph, nullptr, nullptr, 0) != hipSuccess)
+				rc = fail(RT_ERR_DEVICE, "hipGraphInstantiate failed");
+			if (graph) (void)hipGraphDestroy(graph);
+			if (rc) return rc;
+		}
+		ln.plans.push_back(pl);
+		return RT_OK;
+	}
+
 	int start_chunk(Lane& ln, Job& job, int64_t r0, int64_t rows) {
 		const rt_render_params* p = job.p;
 		ln.job = &job;
@@ -360,6 +571,25 @@ struct Render {
 		ln.level_n.assign(1, ln.n0);
 		ln.shaded.clear();
 		ln.deferred.clear();
+		ln.planned = nullptr;
+		if (Plan* pl = find_plan(ln, key_of(ln, job))) {
+			if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
+			if (pl->exec) {  // graph replay: only the output record changes
+				const int64_t W = job.W;
+				ln.jobio_pin->out = job.out_rgb_dev ? job.out_rgb_dev + r0 * W * 3 : nullptr;
+				ln.jobio_pin->out8 = job.out_rgb8_dev ? job.out_rgb8_dev + r0 * W * 3 : nullptr;
+				HIP_TRY(hipMemcpyAsync(ln.jobio_dev, ln.jobio_pin, sizeof(rtamd::JobIO), hipMemcpyHostToDevice,
+				                       ln.stream));
+				HIP_TRY(hipGraphLaunch(pl->exec, ln.stream));
+			} else {
+				const int rc = issue_plan(ln, job, *pl, false);
+				if (rc) return rc;
+			}
+			HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
+			ln.planned = pl;
+			ln.phase = Lane::FINISHING;
+			return RT_OK;
+		}
 		ln.phase = Lane::TRACING;
 		int rc = ensure_level_record(s, ln, 0, ln.n0);
 		if (!rc) rc = launch_closest_level(ln, 0, ln.n0, nullptr);
@@ -375,7 +605,6 @@ struct Render {
 		const Job& job = *ln.job;
 		const int depth = job.depth;
 		const int L = ln.level;
-		cnt.trace_rays += ln.level_n[L];
 		const int64_t nh = ln.counts_host[2 * L], nn = ln.counts_host[2 * L + 1];
 		int rc;
 		// k_closest(L+1) is already queued; queue k_closest(L+2) behind it
@@ -402,12 +631,13 @@ struct Render {
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
 		// colours reduced bottom-up; level 0's reduction is fused into the output
 		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 1; l--)
-			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], ln.levels[l].lv, ln.levels[l + 1].lv, ln.stream));
+			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], nullptr, ln.levels[l].lv, ln.levels[l + 1].lv,
+			                                   ln.stream));
 		const int64_t W = job.W;
 		HIP_TRY(rtamd::launch_output(ln.n0, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
 		                             job.out_rgb_dev ? job.out_rgb_dev + ln.r0 * W * 3 : nullptr,
-		                             job.out_rgb8_dev ? job.out_rgb8_dev + ln.r0 * W * 3 : nullptr, job.io, s->stats,
-		                             ln.stream));
+		                             job.out_rgb8_dev ? job.out_rgb8_dev + ln.r0 * W * 3 : nullptr, nullptr, job.io,
+		                             s->stats, ln.stream));
 		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
 		ln.phase = Lane::FINISHING;
 		return RT_OK;
@@ -416,6 +646,21 @@ struct Render {
 	// the chunk's work is complete: per-kernel device times (events are re-recorded by
 	// the lane's next chunk)
 	int on_done(Lane& ln) {
+		if (ln.planned) {  // a replayed plan: no per-kernel events (its stage times are not measured)
+			const Plan& pl = *ln.planned;
+			for (int k = 0; k < 3; k++) cnt.stage_launches[k] += pl.launches[k];
+			cnt.levels = std::max<int32_t>(cnt.levels, pl.n_levels);
+			cnt.pixels += ln.n0;
+			ln.planned = nullptr;
+			ln.phase = Lane::IDLE;
+			ln.job = nullptr;
+			if (progress) progress->done += ln.n0;
+			return RT_OK;
+		}
+		if (s->graphs && !s->serial && !find_plan(ln, key_of(ln, *ln.job))) {
+			const int rc = build_plan(ln, *ln.job);
+			if (rc) return rc;
+		}
 		for (int L = 0; L < static_cast<int>(ln.level_n.size()); L++) {
 			float ms = 0.f;
 			HIP_TRY(hipEventElapsedTime(&ms, ln.level_events[L][0], ln.level_events[L][1]));
@@ -698,6 +943,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
 	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);
+	if (const char* gr = std::getenv("RTAMD_GRAPH")) s->graphs = std::atoi(gr);
+	if (const char* pt = std::getenv("RTAMD_PLAN_TRUNCATE")) s->plan_truncate = std::atoi(pt);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
@@ -804,12 +1051,28 @@ void reset_after_error(rt_scene* s) {
 	(void)hipGetLastError();
 }
 
+constexpr int kPlanMiss = 1;  // internal return code of render_jobs_impl (never returned by the ABI)
+
 int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
                      Progress* progress);
 
 int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
                 Progress* progress = nullptr) {
-	const int rc = render_jobs_impl(s, jobs, caller, counters, progress);
+	int rc = render_jobs_impl(s, jobs, caller, counters, progress);
+	if (rc == kPlanMiss) {
+		// a replayed plan did not fit (DERR_PLAN: a level it lacked, or a level larger than
+		// its buffer; nothing was written past a buffer): forget the plans and render the
+		// whole call again host-driven, which sizes every level from the counts
+		reset_after_error(s);
+		for (auto& ln : s->lanes) clear_plans(*ln);
+		const int graphs = s->graphs;
+		s->graphs = 0;
+		for (Job& j : jobs) j.next_row = 0;
+		if (progress) progress->done = 0;
+		rc = render_jobs_impl(s, jobs, caller, counters, progress);
+		s->graphs = graphs;
+		if (rc == kPlanMiss) rc = fail(RT_ERR_DEVICE, "internal: level capacity exceeded in a host-driven render");
+	}
 	// a device MathException is reported after a complete render (nothing in flight, the
 	// statistics already cleared by k_stats_finish); any other error may leave work queued
 	if (rc && rc != RT_ERR_MATH) {
@@ -882,8 +1145,10 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	                       hipMemcpyDeviceToHost, caller));
 	HIP_TRY(hipStreamSynchronize(caller));
 	const unsigned long long* sum = s->summary_host;
+	if (sum[rtamd::ST_COUNT] == rtamd::DERR_PLAN) return kPlanMiss;
 	if (sum[rtamd::ST_COUNT]) return fail(RT_ERR_MATH, device_error_text(static_cast<int>(sum[rtamd::ST_COUNT])));
 	rt_counters& cnt = R.cnt;
+	cnt.trace_rays = static_cast<int64_t>(sum[rtamd::ST_RAYS]);
 	cnt.shadow_rays = static_cast<int64_t>(sum[rtamd::ST_HITS]) * s->ds.n_nonambient;
 	cnt.reflect_rays = static_cast<int64_t>(sum[rtamd::ST_REFL]);
 	cnt.refract_rays = static_cast<int64_t>(sum[rtamd::ST_REFR]);

@@ -97,6 +97,8 @@ enum DeviceError : int32_t {
 	DERR_POINT_DIRECTION = 2,   // "ray direction is a point vector"
 	DERR_STACK = 3,             // traversal stack overflow (internal)
 	DERR_ORIGIN_DIRECTION = 4,  // "ray origin is a direction vector" (camera eye with w == 0)
+	DERR_PLAN = 5,              // a replayed launch plan did not fit the render (level capacity or
+	                            // depth): nothing was written past a buffer, the host redoes it
 };
 
 }  // namespace rtamd

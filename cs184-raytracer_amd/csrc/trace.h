@@ -71,6 +71,7 @@ enum StatSlot : int {
 	ST_ENTRIES0, ST_ENTRIES1,                      // LBVH traversals started
 	ST_MAXNODES0, ST_MAXNODES1,                    // most node visits of one ray (max)
 	ST_SHADOW_ZERO,                                // shadow rays whose Phong terms are zero (not traced)
+	ST_RAYS,                                       // rays traced by k_closest (traceRay calls)
 	ST_COUNT
 };
 constexpr int kStatStride = 32;  // u64 per shard (256 B)
@@ -89,9 +90,11 @@ enum : int {
 // n: the level's ray count (level 0), or with n_dev (the previous level's child counter,
 // read on the device) an upper bound used only to size the grid.  levels_dev: the device
 // copy of the RayLevel records (level and level + 1 must be current).
+// plan_last: the last level of a replayed plan (api.cpp): a child spawned there raises
+// DERR_PLAN instead of being written (the plan had no further level for it)
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
                           int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
-                          unsigned long long* stats, hipStream_t stream, int packet_mask);
+                          unsigned long long* stats, hipStream_t stream, int packet_mask, int plan_last = 0);
 // Shading of one or more levels in one launch (the deep levels are shaded together once
 // the closest-hit chain has finished).  Items of each level start on a wave boundary so
 // that every wave belongs to one level.  levels_dev: device copy of the RayLevel records.
@@ -104,6 +107,18 @@ struct ShadeBatch {
 	int32_t fused;                       // all_lights only: k_shadow also computes the Phong terms (no k_shade)
 	int64_t shadow_begin[kMaxBatch + 1]; // k_shadow item ranges: (all_lights ? 1 : n_nonambient) x nh rounded up to 64
 	int64_t shade_begin[kMaxBatch + 1];  // k_shade item ranges: nh each
+	// Device-counted batch (the hipGraph plans of api.cpp): nh[k] is the level's hit counter
+	// nh_dev[k][0], read by the kernels, which derive the item ranges themselves; the grid is
+	// fixed and strides over the items.  nh / shadow_begin / shade_begin are then unused.
+	int32_t dev_counts;
+	const int32_t* nh_dev[kMaxBatch];
+};
+
+// Output pointers of a chunk read by k_output from device memory (a graph replays one
+// launch sequence for every frame; only this record changes)
+struct JobIO {
+	double* out;
+	uint8_t* out8;
 };
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
                          unsigned long long* stats, hipStream_t stream, int packet_mask);
@@ -111,10 +126,15 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 bool shadow_can_fuse(const ShadeBatch& b, int packet_mask);
 hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
                         DeviceCounters* ctr, hipStream_t stream);
-hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream);
-// lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output
+// n: the level's ray count, or with n_dev (the previous level's child counter) read on the
+// device (a fixed grid strides over it)
+hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,
+                               hipStream_t stream);
+// lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output;
+// io_ptrs non-null: the output pointers are read from it (out_rgb / out_rgb8 ignored)
 hipError_t launch_output(int64_t n, const RayLevel& lvl0, const RayLevel* lvl1, double* out_rgb, uint8_t* out_rgb8,
-                         int32_t intersection_only, unsigned long long* stats, hipStream_t stream);
+                         const JobIO* io_ptrs, int32_t intersection_only, unsigned long long* stats,
+                         hipStream_t stream);
 // End of a render: summary[k] = sum over the shards of statistic k (max for ST_MAX_BITS),
 // summary[ST_COUNT] = the device error word; the shards and the error word are cleared for
 // the next render.

@@ -201,7 +201,7 @@ __device__ __forceinline__ Slots block_append2(bool a, bool b0, bool b1, int32_t
 // calls it (block_append2 synchronises the block).
 template <bool kPacket, typename LV>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
-                                             int remaining, const LV& cur, const LV& next,
+                                             int remaining, int plan_last, const LV& cur, const LV& next,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
                                              AppendLds& append_lds, int32_t* stack, uint32_t* stat_lds) {
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
@@ -280,6 +280,14 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 		return;
 	}
 	int32_t refr_idx = -1, refl_idx = -1;
+	// the next level holds at most next.capacity rays: a child beyond it is not written and
+	// the render is flagged (the host redoes it host-driven, api.cpp)
+	// (plan_last: the last level of a replayed plan, whose children were never expected)
+	if ((spawn_refr || spawn_refl) &&
+	    (plan_last || slot.b + (spawn_refr && spawn_refl ? 1 : 0) >= next.capacity)) {
+		raise_error(ctr, DERR_PLAN);
+		spawn_refr = spawn_refl = false;
+	}
 	if (spawn_refr) {
 		refr_idx = slot.b;
 		next.ox[refr_idx] = P.x;
@@ -332,8 +340,8 @@ template <bool kPacket>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
                                                                       int64_t n_host, const int32_t* n_dev,
-                                                                      int remaining, const RayLevel* levels,
-                                                                      DeviceCounters* ctr,
+                                                                      int remaining, int plan_last,
+                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                       unsigned long long* stats) {
 	__shared__ AppendLds append_lds;
 	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
@@ -342,14 +350,19 @@ __global__ void __launch_bounds__(kBlock)
 	// level records read through the constant address space (scalar loads at their uses)
 	const auto& cur = *uniform_ptr(levels + level);
 	const auto& next = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
-	// the next level's counts start at zero (its k_closest appends to them)
-	if (remaining > 0 && blockIdx.x == 0 && threadIdx.x == 0) next.counts[0] = next.counts[1] = 0;
-	const int64_t n = n_dev ? static_cast<int64_t>(*n_dev) : n_host;
+	// the level's rays: n_host, or the previous level's child counter, never more than the
+	// level holds (children beyond its capacity were not written, see closest_item)
+	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur.capacity) : n_host;
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		// the next level's counts start at zero (its k_closest appends to them)
+		if (remaining > 0) next.counts[0] = next.counts[1] = 0;
+		if (n) atomicAdd(stats + ST_RAYS, static_cast<unsigned long long>(n));  // traceRay calls
+	}
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride)
-		closest_item<kPacket>(S, fg, level, n, remaining, cur, next, ctr, stats, base + threadIdx.x, append_lds, stack,
-		                      stat_lds);
+		closest_item<kPacket>(S, fg, level, n, remaining, plan_last, cur, next, ctr, stats, base + threadIdx.x,
+		                      append_lds, stack, stat_lds);
 }
 
 // Level of item t of a batch (wave-uniform: every level's items start on a wave boundary,
@@ -358,12 +371,44 @@ struct BatchItem {
 	int32_t level;
 	int64_t local, nh;
 };
-__device__ __forceinline__ BatchItem batch_item(const ShadeBatch& B, const int64_t* begin, int64_t t) {
-const int64_t t0 = __builtin_amdgcn_readfirstlane(static_cast<int32_t>(t & ~int64_t(63))) |
-(static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int32_t>(t >> 32))) << 32);
-int k = 0;
-while (k + 1 < B.n && t0 >= begin[k + 1]) k++;
-return BatchItem{B.level[k], t - begin[k], B.nh[k]};
+__device__ __forceinline__ int64_t wave_first(int64_t t) {
+	return __builtin_amdgcn_readfirstlane(static_cast<int32_t>(t & ~int64_t(63))) |
+	       (static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int32_t>(t >> 32))) << 32);
+}
+__device__ __forceinline__ int64_t wave_up64(int64_t x) { return (x + 63) & ~int64_t(63); }
+// hits of level k of a device-counted batch (its k_closest has completed)
+__device__ __forceinline__ int64_t batch_nh(const ShadeBatch& B, int k) { return *uniform_ptr(B.nh_dev[k]); }
+// items per hit: k_shadow (all lights: 1, light-major: one per non-ambient light) or k_shade (1)
+template <bool kShadow>
+__device__ __forceinline__ int64_t batch_items_per_hit(const ShadeBatch& B, int nl) {
+	return (kShadow && !B.all_lights) ? nl : 1;
+}
+template <bool kShadow>
+__device__ __forceinline__ BatchItem batch_item(const ShadeBatch& B, int nl, int64_t t) {
+	const int64_t t0 = wave_first(t);
+	if (!B.dev_counts) {
+		const int64_t* begin = kShadow ? B.shadow_begin : B.shade_begin;
+		int k = 0;
+		while (k + 1 < B.n && t0 >= begin[k + 1]) k++;
+		return BatchItem{B.level[k], t - begin[k], B.nh[k]};
+	}
+	// ranges from the levels' hit counters: level k covers items_per_hit x nh rounded up to 64
+	const int64_t per = batch_items_per_hit<kShadow>(B, nl);
+	int64_t begin = 0, nh = batch_nh(B, 0);
+	int k = 0;
+	while (k + 1 < B.n && t0 >= begin + per * wave_up64(nh)) {
+		begin += per * wave_up64(nh);
+		nh = batch_nh(B, ++k);
+	}
+	return BatchItem{B.level[k], t - begin, nh};
+}
+// items of the whole batch
+template <bool kShadow>
+__device__ __forceinline__ int64_t batch_total(const ShadeBatch& B, int nl) {
+	if (!B.dev_counts) return kShadow ? B.shadow_begin[B.n] : B.shade_begin[B.n];
+	int64_t tot = 0;
+	for (int k = 0; k < B.n; k++) tot += batch_items_per_hit<kShadow>(B, nl) * wave_up64(batch_nh(B, k));
+	return tot;
 }
 
 // Phong terms in light order (scene.cpp:78-108) of hit slot hs (hit point P, shading normal
@@ -420,19 +465,14 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 //    records once for all lights.
 // The light record of the wave is read with scalar loads.
 template <bool kPacket>
-__global__ void __launch_bounds__(kBlock)
-    __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
-                                                                     const RayLevel* levels, DeviceCounters* ctr,
-                                                                     unsigned long long* stats) {
-	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
-	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	const int64_t tg = xcd_block() * kBlock + threadIdx.x;
-	const BatchItem it = batch_item(B, B.shadow_begin, tg);
+__device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
+                                            DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
+                                            uint32_t* stat_lds) {
+	const int nl = S.n_nonambient;
+	const BatchItem it = batch_item<true>(B, nl, tg);
 	const int level = it.level;
 	const int64_t t = it.local, nh = it.nh;
 	const auto& cur = *uniform_ptr(levels + level);
-	const int nl = S.n_nonambient;
-	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
 	WorkStats ws{};
 	ws.init(stat_lds);
 	PROF_BEGIN(t_total);
@@ -507,6 +547,22 @@ __global__ void __launch_bounds__(kBlock)
 		          glibc_pow_data::kExpTab, ctr);
 }
 
+// Host-counted batches launch one thread per item; device-counted ones a fixed grid that
+// strides over the items (the bound is block-uniform: no lane of a wave leaves early).
+template <bool kPacket>
+__global__ void __launch_bounds__(kBlock)
+    __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
+                                                                     const RayLevel* levels, DeviceCounters* ctr,
+                                                                     unsigned long long* stats) {
+	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
+	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	const int64_t total = batch_total<true>(B, S.n_nonambient);
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
+		shadow_item<kPacket>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
+}
+
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
 __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeometry fg, ShadeBatch B,
                                                        const RayLevel* levels, DeviceCounters* ctr) {
@@ -517,16 +573,20 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeome
 	for (int k = threadIdx.x; k < 512; k += blockDim.x) log_tab[k] = glibc_pow_data::kLogTab[k];
 	for (int k = threadIdx.x; k < 256; k += blockDim.x) exp_tab[k] = glibc_pow_data::kExpTab[k];
 	__syncthreads();
-	const BatchItem it = batch_item(B, B.shade_begin, xcd_block() * blockDim.x + threadIdx.x);
-	if (it.local >= it.nh) return;
-	const int level = it.level;
-	const auto& cur = *uniform_ptr(levels + level);
-	const int64_t hs = it.local;  // the hit's slot (hit records, verdicts)
-	const V3 d = mk(cur.hdx[hs], cur.hdy[hs], cur.hdz[hs]);  // the viewing ray's direction
-	const V3 P = mk(cur.hpx[hs], cur.hpy[hs], cur.hpz[hs]);
-	const V3 N = mk(cur.hnx[hs], cur.hny[hs], cur.hnz[hs]);
-	shade_hit(S, cur, hs, P, N, d, [&](int j) { return static_cast<bool>(cur.occl[j * cur.capacity + hs]); }, log_tab,
-	          exp_tab, ctr);
+	const int64_t total = batch_total<false>(B, S.n_nonambient);
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+	for (int64_t base = xcd_block() * blockDim.x; base < total; base += stride) {
+		const BatchItem it = batch_item<false>(B, S.n_nonambient, base + threadIdx.x);
+		if (it.local >= it.nh) continue;
+		const int level = it.level;
+		const auto& cur = *uniform_ptr(levels + level);
+		const int64_t hs = it.local;  // the hit's slot (hit records, verdicts)
+		const V3 d = mk(cur.hdx[hs], cur.hdy[hs], cur.hdz[hs]);  // the viewing ray's direction
+		const V3 P = mk(cur.hpx[hs], cur.hpy[hs], cur.hpz[hs]);
+		const V3 N = mk(cur.hnx[hs], cur.hny[hs], cur.hnz[hs]);
+		shade_hit(S, cur, hs, P, N, d, [&](int j) { return static_cast<bool>(cur.occl[j * cur.capacity + hs]); },
+		          log_tab, exp_tab, ctr);
+	}
 }
 
 // colour = (local + refraction) + reflection * kr, in place (scene.cpp:127,134)
@@ -546,15 +606,17 @@ __device__ __forceinline__ void reduce_colour(int64_t i, const RayLevel& cur, co
 		c[2] = c[2] + next.cb[r] * cur.kb[i];
 	}
 }
-__global__ void k_reduce(int64_t n, RayLevel cur, RayLevel next) {
-	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (i >= n) return;
-	if (cur.child_refr[i] < 0 && cur.child_refl[i] < 0) return;
-	double c[3];
-	reduce_colour(i, cur, next, c);
-	cur.cr[i] = c[0];
-	cur.cg[i] = c[1];
-	cur.cb[i] = c[2];
+__global__ void k_reduce(int64_t n_host, const int32_t* n_dev, RayLevel cur, RayLevel next) {
+	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur.capacity) : n_host;
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+		if (cur.child_refr[i] < 0 && cur.child_refl[i] < 0) continue;
+		double c[3];
+		reduce_colour(i, cur, next, c);
+		cur.cr[i] = c[0];
+		cur.cg[i] = c[1];
+		cur.cb[i] = c[2];
+	}
 }
 
 // writers.cpp:4-9: (uint8)(min(max(v,0),1) * 255), NaN -> 0
@@ -567,9 +629,13 @@ __device__ __forceinline__ uint8_t to_u8(double v) {
 
 // the image: level 0's colours, reduced with level 1 on the fly when `reduce` (the last
 // k_reduce fused into the output)
-__global__ void k_output(int64_t n, RayLevel lvl0, RayLevel lvl1, int32_t reduce, double* out, uint8_t* out8, int32_t io,
-                         unsigned long long* stats) {
+__global__ void k_output(int64_t n, RayLevel lvl0, RayLevel lvl1, int32_t reduce, double* out, uint8_t* out8,
+                         const JobIO* io_ptrs, int32_t io, unsigned long long* stats) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+	if (io_ptrs) {
+		out = uniform_ptr(io_ptrs)->out;
+		out8 = uniform_ptr(io_ptrs)->out8;
+	}
 	// level 0's counts were read back; clear them for the lane's next chunk
 	if (i == 0) lvl0.counts[0] = lvl0.counts[1] = 0;
 	double v[3] = {0, 0, 0};
@@ -657,7 +723,7 @@ constexpr int64_t kStrideBlocks = 256 * 8;
 
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
                           int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
-                          unsigned long long* stats, hipStream_t stream, int packet_mask) {
+                          unsigned long long* stats, hipStream_t stream, int packet_mask, int plan_last) {
 	if (n <= 0) return hipSuccess;
 	const bool packet = packet_mask & (level == 0 ? kPacketClosest0 : level == 1 ? kPacketClosestN | kPacketClosest1 : kPacketClosestN);
 	const int64_t threads = (level == 0 && packet) ? tile_threads(n, fg.width) : n;
@@ -666,10 +732,10 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 	                            : grid_for(threads, kBlock);
 	if (packet)
 		hipLaunchKernelGGL(k_closest<true>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
-		                   levels_dev, ctr, stats);
+		                   plan_last, levels_dev, ctr, stats);
 	else
 		hipLaunchKernelGGL(k_closest<false>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev,
-		                   remaining_depth, levels_dev, ctr, stats);
+		                   remaining_depth, plan_last, levels_dev, ctr, stats);
 	return hipGetLastError();
 }
 
@@ -680,39 +746,49 @@ static bool shadow_packet(const ShadeBatch& b, int packet_mask) {
 
 bool shadow_can_fuse(const ShadeBatch& b, int packet_mask) { return b.all_lights && shadow_packet(b, packet_mask); }
 
+// grid of a device-counted batch: one thread per item of `bound` (an upper bound of its
+// items, from the levels' capacities); the blocks beyond the device count exit at once
+#ifndef RT_DEV_GRID_CAP
+#define RT_DEV_GRID_CAP (1 << 20)
+#endif
+inline unsigned dev_grid(int64_t bound, int block) {
+	return (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(bound, block), RT_DEV_GRID_CAP));
+}
+
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
                          unsigned long long* stats, hipStream_t stream, int packet_mask) {
-	const int64_t items = b.shadow_begin[b.n];
+	const int64_t items = b.shadow_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0 || s.n_nonambient <= 0) return hipSuccess;
+	const unsigned grid = b.dev_counts ? dev_grid(items, kBlock) : grid_for(items, kBlock);
 	if (shadow_packet(b, packet_mask))
-		hipLaunchKernelGGL(k_shadow<true>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, b, levels_dev, ctr,
-		                   stats);
+		hipLaunchKernelGGL(k_shadow<true>, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
 	else
-		hipLaunchKernelGGL(k_shadow<false>, dim3(grid_for(items, kBlock)), dim3(kBlock), 0, stream, s, b, levels_dev,
-		                   ctr, stats);
+		hipLaunchKernelGGL(k_shadow<false>, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
 	return hipGetLastError();
 }
 
 hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
                         DeviceCounters* ctr, hipStream_t stream) {
-	const int64_t items = b.shade_begin[b.n];
+	const int64_t items = b.shade_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0) return hipSuccess;
-	hipLaunchKernelGGL(k_shade, dim3(grid_for(items, kShadeBlock)), dim3(kShadeBlock), 0, stream, s, fg, b, levels_dev,
-	                   ctr);
+	const unsigned grid = b.dev_counts ? dev_grid(items, kShadeBlock) : grid_for(items, kShadeBlock);
+	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, fg, b, levels_dev, ctr);
 	return hipGetLastError();
 }
 
-hipError_t launch_reduce_level(int64_t n, const RayLevel& cur, const RayLevel& next, hipStream_t stream) {
+hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,
+                               hipStream_t stream) {
 	if (n <= 0) return hipSuccess;
-	hipLaunchKernelGGL(k_reduce, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, cur, next);
+	const unsigned grid = n_dev ? dev_grid(n, 256) : grid_for(n, 256);
+	hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, stream, n, n_dev, cur, next);
 	return hipGetLastError();
 }
 
 hipError_t launch_output(int64_t n, const RayLevel& lvl0, const RayLevel* lvl1, double* out_rgb, uint8_t* out_rgb8,
-                         int32_t io, unsigned long long* stats, hipStream_t stream) {
+                         const JobIO* io_ptrs, int32_t io, unsigned long long* stats, hipStream_t stream) {
 	if (n <= 0) return hipSuccess;
 	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, lvl0, lvl1 ? *lvl1 : lvl0,
-	                   lvl1 ? 1 : 0, out_rgb, out_rgb8, io, stats);
+	                   lvl1 ? 1 : 0, out_rgb, out_rgb8, io_ptrs, io, stats);
 	return hipGetLastError();
 }
 

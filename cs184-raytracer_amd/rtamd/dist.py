@@ -31,6 +31,8 @@ def n_rows(height: int, rank: int, world: int) -> int:
 
 def global_max(value: float, device: torch.device) -> float:
     """All-reduce MAX of a scalar (the --intersection-only normaliser)."""
+    if dist.is_initialized() and dist.get_backend() == "gloo":
+        device = torch.device("cpu")  # gloo reduces host tensors
     t = torch.tensor([value], dtype=torch.float64, device=device)
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -38,37 +40,65 @@ def global_max(value: float, device: torch.device) -> float:
 
 
 def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
-                out: Optional[torch.Tensor] = None, bufs: Optional[list] = None, shift: int = 0) -> Optional[torch.Tensor]:
+                out: Optional[torch.Tensor] = None, bufs: Optional[list] = None, shift: int = 0,
+                group=None, group_size: Optional[int] = None,
+                group_rank: Optional[int] = None) -> Optional[torch.Tensor]:
     """Gathers every rank's interleaved rows (n_local, W, C) into a (H, W, C) frame on `dst`
-    (rank r holds rows (r + shift) mod world, see rank_rows)."""
-    world = dist.get_world_size() if dist.is_initialized() else 1
-    rank = dist.get_rank() if dist.is_initialized() else 0
+    (rank r holds rows (r + shift) mod world, see rank_rows).  `local` may be longer than the
+    rank's row count (a buffer of the longest rank's rows): the extra rows are ignored.
+    With `group` (a sub-communicator of ranks 0 .. group_size - 1), world = group_size and
+    the rank is group_rank; `dst` is a global rank inside the group."""
+    world = group_size if group is not None else (dist.get_world_size() if dist.is_initialized() else 1)
+    rank = group_rank if group is not None else (dist.get_rank() if dist.is_initialized() else 0)
     if world == 1:
+        rows = local[: height]
         if out is None:
-            return local.clone()
-        out.copy_(local)
+            return rows.clone()
+        out.copy_(rows)
         return out
     n_max = -(-height // world)
     if not local.is_contiguous():
         local = local.contiguous()
     if local.shape[0] != n_max:
         pad = torch.zeros((n_max,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-        pad[: local.shape[0]] = local
+        k = min(n_max, local.shape[0])
+        pad[:k] = local[:k]
         local = pad
-    staged = local.is_cuda and dist.get_backend() == "gloo"  # gloo gathers host tensors
+    staged = local.is_cuda and dist.get_backend(group) == "gloo"  # gloo gathers host tensors
     if staged:
         local = local.cpu()
     if rank == dst:
         if bufs is None or staged:
             bufs = [torch.empty_like(local) for _ in range(world)]
-        dist.gather(local, bufs, dst=dst)
+        dist.gather(local, bufs, dst=dst, group=group)
         if out is None:
             out = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         for r in range(world):
             k = (r + shift) % world
             out[k::world] = bufs[r][: n_rows(height, k, world)].to(out.device)
         return out
-    dist.gather(local, None, dst=dst)
+    dist.gather(local, None, dst=dst, group=group)
+    return None
+
+
+def gather_frames(frame: torch.Tensor, dst: int = 0, out: Optional[list] = None) -> Optional[list]:
+    """Frame-parallel mode: every rank's whole frame to `dst` (out[r] = rank r's frame)."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if world == 1:
+        if out is not None:
+            out[0].copy_(frame)
+        return out
+    staged = frame.is_cuda and dist.get_backend() == "gloo"
+    src = frame.cpu() if staged else frame.contiguous()
+    if rank == dst:
+        bufs = [torch.empty_like(src) for _ in range(world)] if staged or out is None else list(out)
+        dist.gather(src, bufs, dst=dst)
+        if out is not None and staged:
+            for r in range(world):
+                out[r].copy_(bufs[r])
+        return out if out is not None else bufs
+    dist.gather(src, None, dst=dst)
     return None
 
 

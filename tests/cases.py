@@ -5,9 +5,11 @@ copied under scenes/) plus the two authored config scenes of SURVEY.md App. B.
 """
 import glob
 import os
+import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SCENES = os.path.join(REPO, "scenes")
+sys.path.insert(0, os.path.join(REPO, "cs184-raytracer_amd"))
 
 
 def scene_files():
@@ -28,30 +30,8 @@ OPTION_SETS = [
 ]
 
 
-def option_kwargs(flags):
-    bdepth, io = 10, False
-    i = 0
-    while i < len(flags):
-        if flags[i] == "--bdepth":
-            bdepth = int(flags[i + 1])
-            i += 2
-        elif flags[i] == "--intersection-only":
-            io = True
-            i += 1
-        else:
-            raise ValueError(flags[i])
-    return {"bdepth": bdepth, "intersection_only": io}
+from rtamd.configs import CONFIGS, option_kwargs  # noqa: E402,F401  (BASELINE.json configs, shared with bench.py)
 
-
-# BASELINE.json configs: name -> (scene, W, H, flags)
-CONFIGS = {
-    "C1_simple_sphere_256": ("excess_inputs/simple_sphere.rti", 256, 256, []),
-    "C2a_input01_1024_bd0": ("inputs/input-01.rti", 1024, 1024, ["--bdepth", "0"]),
-    "C2b_input02_teapot_1024_bd0": ("inputs/input-02.rti", 1024, 1024, ["--bdepth", "0"]),
-    "C3_bunny_1920x1080_bd4": ("excess_inputs/bunny.rti", 1920, 1080, ["--bdepth", "4"]),
-    "C4_airboat_sub_1920x1080": ("excess_inputs/minicooper_sub.rti", 1920, 1080, []),
-    "C5_refraction3_4096_bd8": ("excess_inputs/refraction3.rti", 4096, 4096, ["--bdepth", "8"]),
-}
 
 # The reference's shipped renders (outputs/image-0N.png, notes/notes-0N.txt:3)
 SHIPPED = {f"image-0{i}.png": (f"inputs/input-0{i}.rti", 2000 if i == 9 else 1000, 2000 if i == 9 else 1000)

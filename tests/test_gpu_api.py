@@ -128,11 +128,12 @@ def test_many_lights(gpu, oracle, tmp_path):
     s.close()
 
 
-@pytest.mark.parametrize("after", [0, 1, 3])
-def test_render_after_a_failed_render_is_exact(gpu, oracle, after):
+@pytest.mark.parametrize("after,graph", [(0, "1"), (0, "0"), (1, "0"), (3, "0")])
+def test_render_after_a_failed_render_is_exact(gpu, oracle, after, graph, monkeypatch):
     """A device failure in the middle of a render (injected after `after` closest-hit
-    launches) returns an error; the scene's next render is complete, bit-exact and counts
-    exactly its own rays (no stale lane, counter or error word)."""
+    launches; a replayed plan counts as one) returns an error; the scene's next render is
+    complete, bit-exact and counts exactly its own rays (no stale lane, counter or error word)."""
+    monkeypatch.setenv("RTAMD_GRAPH", graph)
     scene = "excess_inputs/bunny.rti"
     w, h, bdepth = 80, 45, 4
     want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
@@ -177,3 +178,66 @@ def test_camera_eye_direction_vector_raises(gpu):
         s.renderScene(options=gpu.Options(renderWidth_=8, renderHeight_=8))
     s.close()
     src.close()
+
+
+@pytest.mark.parametrize("scene,bdepth,chunk", [("excess_inputs/bunny.rti", 4, 0), ("excess_inputs/refraction3.rti", 8, 0),
+                                                ("excess_inputs/refraction3.rti", 8, 900), ("inputs/input-06.rti", 10, 0),
+                                                ("inputs/input-09.rti", 10, 1500)])
+@pytest.mark.parametrize("graph", ["0", "1", "2"])
+def test_replayed_plans_are_exact(gpu, oracle, scene, bdepth, chunk, graph, monkeypatch):
+    """Launch plans (hipGraph replay of a traced chunk shape, device-read level sizes): the
+    2nd and 3rd renders of the same shape replay the plan; every render is bit-exact with
+    the oracle and counts the reference's rays."""
+    monkeypatch.setenv("RTAMD_GRAPH", graph)
+    w, h = 90, 50
+    want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth)
+    for _ in range(3):
+        img = s.renderScene(options=o, chunk_pixels=chunk)
+        assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
+        assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+        assert (s.last_stats.reflect_rays, s.last_stats.refract_rays) == (cnt["reflect_rays"], cnt["refract_rays"])
+    s.close()
+
+
+@pytest.mark.parametrize("graph", ["1", "2"])
+def test_replayed_plan_batch_and_rgb8(gpu, monkeypatch, graph):
+    """A batch of frames over three lanes (each lane builds, then replays, its plan) with
+    f64 and RGB8 outputs (graph replay: written through the plans' output records)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("RTAMD_GRAPH", graph)
+    scene = "excess_inputs/bunny.rti"
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    w, h = 96, 54
+    ref = s.renderScene(options=gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=4))
+    prm = s.params(w, h, 4, False)
+    for _ in range(3):
+        outs = [torch.full((h, w, 3), -1.0, dtype=torch.float64, device="cuda") for _ in range(7)]
+        out8 = [torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda") for _ in range(7)]
+        torch.cuda.synchronize()
+        s.render_batch_device([prm] * 7, [o.data_ptr() for o in outs], [o.data_ptr() for o in out8])
+        for k in range(7):
+            assert np.array_equal(outs[k].cpu().numpy(), ref), k
+            assert np.array_equal(out8[k].cpu().numpy(), gpu.to_rgb8(ref)), k
+    s.close()
+
+
+@pytest.mark.parametrize("graph", ["1", "2"])
+@pytest.mark.parametrize("scene,bdepth,io", [("excess_inputs/refraction3.rti", 8, False), ("inputs/input-05.rti", 10, False),
+                                             ("inputs/input-02.rti", 10, True)])
+def test_plan_miss_is_redone_exactly(gpu, oracle, scene, bdepth, io, graph, monkeypatch):
+    """A plan one level short (RTAMD_PLAN_TRUNCATE test hook): its replay raises DERR_PLAN
+    on the device instead of writing the unplanned children, and the render is redone
+    host-driven: still bit-exact, counters exact."""
+    monkeypatch.setenv("RTAMD_PLAN_TRUNCATE", "1")
+    monkeypatch.setenv("RTAMD_GRAPH", graph)
+    w, h = 64, 40
+    want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth, intersection_only=io)
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth, intersectionOnly_=io)
+    for _ in range(3):
+        img = s.renderScene(options=o)
+        assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
+        assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+    s.close()
