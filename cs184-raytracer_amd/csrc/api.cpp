@@ -1433,6 +1433,36 @@ int rt_debug_builder_digest(const rt_builder* b, uint64_t* out) {
 	return RT_OK;
 }
 
+// Diagnostic (not in rtamd.h): FETCH_SIZE calibration.  Reads a fresh `bytes` buffer once per
+// width in {1, 4, 8, 16} bytes per lane (one k_stream_read dispatch each, after a dispatch
+// that streams another buffer of the same size through the caches); profiled with
+// rocprofv3 --pmc FETCH_SIZE, the ratio of the counter to `bytes` per width corrects the
+// path's own loads (tools/make_traffic.py).
+int rt_debug_fetch_calibration(int device, int64_t bytes) {
+	HIP_TRY(hipSetDevice(device));
+	struct Buffers {
+		void* p[3] = {nullptr, nullptr, nullptr};
+		~Buffers() {
+			for (void* q : p)
+				if (q) (void)hipFree(q);
+		}
+	} b;
+	HIP_TRY(hipMalloc(&b.p[0], bytes));
+	HIP_TRY(hipMalloc(&b.p[1], bytes));
+	HIP_TRY(hipMalloc(&b.p[2], 64));
+	HIP_TRY(hipMemset(b.p[0], 0, bytes));
+	HIP_TRY(hipMemset(b.p[1], 0, bytes));
+	HIP_TRY(hipDeviceSynchronize());
+	const int widths[4] = {1, 4, 8, 16};
+	for (int w : widths) {
+		// evict: stream the other buffer first (larger than the 256 MiB Infinity Cache)
+		HIP_TRY(rtamd::launch_stream_read(b.p[1], bytes, 16, static_cast<unsigned long long*>(b.p[2]), nullptr));
+		HIP_TRY(rtamd::launch_stream_read(b.p[0], bytes, w, static_cast<unsigned long long*>(b.p[2]), nullptr));
+		HIP_TRY(hipDeviceSynchronize());
+	}
+	return RT_OK;
+}
+
 // Diagnostic (not in rtamd.h): the scene's next render fails after `launches` more
 // closest-hit launches, as a device failure in the middle of a render would (tests of the
 // error path: the render after it must be complete and exact).  -1 disables.

@@ -715,6 +715,21 @@ __global__ void k_selftest(int op, const double* x, const double* y, double* out
 		out[i] = x[i] / y[i];
 }
 
+// FETCH_SIZE calibration (profiles/, MI355X_MICROARCH.md: the counter is calibrated only
+// for 16-B-per-lane streaming reads): every element of a buffer far larger than the
+// Infinity Cache read once, W bytes per lane per load, coalesced like the ray and hit
+// records (consecutive lanes, consecutive elements)
+template <typename T>
+__global__ void k_stream_read(const T* __restrict__ p, int64_t n, unsigned long long* sink) {
+	unsigned long long acc = 0;
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+		const T v = p[i];
+		acc += reinterpret_cast<const unsigned char*>(&v)[0];
+	}
+	if (acc == 0x7fffffffffffffffull) sink[0] = acc;  // keeps the loads; never true for the zeroed buffer
+}
+
 inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 // grid of the stride loops: 8 blocks (16 waves) per CU, 4 waves per SIMD
 constexpr int64_t kStrideBlocks = 256 * 8;
@@ -815,6 +830,17 @@ hipError_t read_phase_profile(unsigned long long* out) {
 	for (int k = 0; k < 4 * kPhaseSlots; k++) out[k] = 0;
 	return hipSuccess;
 #endif
+}
+
+hipError_t launch_stream_read(const void* buf, int64_t bytes, int width, unsigned long long* sink, hipStream_t stream) {
+	const unsigned grid = 256 * 8;
+	switch (width) {
+		case 1: hipLaunchKernelGGL(k_stream_read<uint8_t>, dim3(grid), dim3(256), 0, stream, (const uint8_t*)buf, bytes, sink); break;
+		case 4: hipLaunchKernelGGL(k_stream_read<uint32_t>, dim3(grid), dim3(256), 0, stream, (const uint32_t*)buf, bytes / 4, sink); break;
+		case 8: hipLaunchKernelGGL(k_stream_read<uint64_t>, dim3(grid), dim3(256), 0, stream, (const uint64_t*)buf, bytes / 8, sink); break;
+		default: hipLaunchKernelGGL(k_stream_read<uint4>, dim3(grid), dim3(256), 0, stream, (const uint4*)buf, bytes / 16, sink); break;
+	}
+	return hipGetLastError();
 }
 
 hipError_t launch_selftest_math(int op, const double* x, const double* y, double* out, int64_t n, hipStream_t stream) {

@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-2 profiling recipe (run on the MI355X box via gpurun): kernel trace + stats of the
+# solo pass (the roofline's time base) and of the default bench, separate PMC passes for
+# HBM bytes (FETCH_SIZE, WRITE_SIZE) over the solo pass, and the FETCH_SIZE calibration.
+#   usage: tools/profile_round2.sh <tag>   then: python tools/make_traffic.py gpurun_out/<tag> profiles/round2
+set -o pipefail
+TAG=${1:-prof2}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/solo -o solo --output-format csv -- python $R/bench.py --solo-only --solo-frames 5 > $O/solo.log 2>&1 || exit 2
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- python $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline > $O/kt.log 2>&1 || exit 3
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o pmc --output-format csv -- python $R/bench.py --solo-only --solo-frames 3 > $O/fetch.log 2>&1 || exit 4
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/write -o pmc --output-format csv -- python $R/bench.py --solo-only --solo-frames 3 > $O/write.log 2>&1 || exit 5
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/calib -o pmc --output-format csv -- python $R/tools/fetch_calibration.py > $O/calib.log 2>&1 || exit 6
+echo done
