@@ -56,14 +56,19 @@ struct rt_builder {
 static_assert(sizeof(rt_face_desc) == sizeof(rtamd::Face) && sizeof(rt_face_desc) == 192,
               "rt_face_desc is Mesh::Face (geometry.h:32) and the host Face");
 
-// One image (or row selection) of a render call: its parameters, outputs and the rows
-// not yet handed to a lane.
+// One image (or row selection) of a render call: its parameters and outputs.
 struct Job {
 	const rt_render_params* p;
 	double* out_rgb_dev;
 	uint8_t* out_rgb8_dev;
 	int depth, io;
-	int64_t W, n_rows, chunk_rows, next_row;
+	int64_t W, n_rows;
+};
+
+// Rows [r0, r0 + rows) of a job's selected rows (ordinals), part of one chunk
+struct Segment {
+	const Job* job;
+	int64_t r0, rows;
 };
 
 // Progress of a render call (scene.cpp:41-44: the calling thread reports completed pixels
@@ -91,11 +96,12 @@ struct LevelBuffers {
 // larger level) is caught on the device (DERR_PLAN, nothing written past a buffer) and the
 // render is redone host-driven.
 struct PlanKey {
-	int32_t width, height, row_begin, row_step, chunk_row0, depth, io;
+	int32_t width, height, depth, io;
 	int64_t n0;
+	uint64_t rows_hash;  // the chunk's image rows (they decide the level counts)
 	bool operator==(const PlanKey& o) const {
-		return width == o.width && height == o.height && row_begin == o.row_begin && row_step == o.row_step &&
-		       chunk_row0 == o.chunk_row0 && depth == o.depth && io == o.io && n0 == o.n0;
+		return width == o.width && height == o.height && depth == o.depth && io == o.io && n0 == o.n0 &&
+		       rows_hash == o.rows_hash;
 	}
 };
 
@@ -134,9 +140,14 @@ struct Lane {
 	int32_t* counts_host = nullptr;      // pinned, per level: hits, children (levels_cap x 2)
 	// chunk state
 	enum Phase { IDLE, TRACING, FINISHING } phase = IDLE;
-	Job* job = nullptr;                   // the render job the chunk belongs to
+	std::vector<Segment> segs;            // the chunk's rows: pieces of one or several jobs
+	int depth = 0, io = 0;                // shared by the chunk's jobs
+	uint64_t rows_hash = 0;               // the image rows of the chunk (plan key)
 	rtamd::FrameGeometry fg{};
-	int64_t r0 = 0, n0 = 0;
+	int64_t n0 = 0;                       // pixels of the chunk (its rows x width)
+	rtamd::ChunkRow* rows_dev = nullptr;  // the chunk's row table (device; FrameGeometry::rows)
+	rtamd::ChunkRow* rows_pin = nullptr;  // its pinned staging (one chunk in flight per lane)
+	int64_t rows_cap = 0;
 	int level = 0;                        // the level whose counts are awaited
 	std::vector<int64_t> level_n;         // ray counts of the levels known so far
 	std::vector<int> shaded;                        // first level of each shading launch
@@ -145,8 +156,6 @@ struct Lane {
 	// buffer is reallocated
 	std::vector<Plan> plans;
 	const Plan* planned = nullptr;        // the plan replaying the current chunk, if any
-	rtamd::JobIO* jobio_dev = nullptr;    // the chunk's output pointers (read by k_output)
-	rtamd::JobIO* jobio_pin = nullptr;    // pinned staging of jobio_dev (one chunk in flight)
 };
 
 void clear_plans(Lane& ln) {
@@ -184,6 +193,7 @@ struct rt_scene {
 	// replayed as hipGraphs, 2 issued directly (default: this ROCm's graph replay serialises
 	// the branches and the lanes)
 	int graphs = 2;
+	int64_t batch_chunk_pixels = (int64_t)1 << 22;  // RTAMD_BATCH_CHUNK: most pixels of a chunk packed from several jobs
 	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
 	int shadow_all_lights = 1;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// measured best on C3: packets for the camera rays and their first bounce, and
@@ -302,15 +312,13 @@ int lane_create(Lane& ln, int prio_low, int prio_high) {
 	HIP_TRY(hipStreamCreateWithPriority(&ln.readback, hipStreamNonBlocking, prio_high));
 	for (hipStream_t& q : ln.shade) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
 	HIP_TRY(hipEventCreateWithFlags(&ln.chunk_done, hipEventDisableTiming));
-	HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ln.jobio_dev), sizeof(rtamd::JobIO)));
-	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.jobio_pin), sizeof(rtamd::JobIO), hipHostMallocDefault));
 	return RT_OK;
 }
 
 void lane_destroy(Lane& ln) {
 	clear_plans(ln);
-	if (ln.jobio_dev) (void)hipFree(ln.jobio_dev);
-	if (ln.jobio_pin) (void)hipHostFree(ln.jobio_pin);
+	if (ln.rows_dev) (void)hipFree(ln.rows_dev);
+	if (ln.rows_pin) (void)hipHostFree(ln.rows_pin);
 	for (auto& L : ln.levels)
 		if (L.block) (void)hipFree(L.block);
 	if (ln.levels_pinned) (void)hipHostFree(ln.levels_pinned);
@@ -338,7 +346,7 @@ struct Render {
 	// with n_dev (the previous level's child counter) an upper bound: the level is queued
 	// behind the previous one before the host knows its size (one level of lookahead).
 	int launch_closest_level(Lane& ln, int L, int64_t n, const int32_t* n_dev) {
-		const int remaining = ln.job->depth - L;
+		const int remaining = ln.depth - L;
 		int rc;
 		// children of this level: at most 2 per ray
 		if (remaining > 0 && (rc = ensure_level_record(s, ln, L + 1, 2 * n))) return rc;
@@ -397,16 +405,14 @@ struct Render {
 		return RT_OK;
 	}
 
-	PlanKey key_of(const Lane& ln, const Job& job) const {
+	PlanKey key_of(const Lane& ln) const {
 		PlanKey k{};
 		k.width = ln.fg.width;
 		k.height = ln.fg.height;
-		k.row_begin = ln.fg.row_begin;
-		k.row_step = ln.fg.row_step;
-		k.chunk_row0 = ln.fg.chunk_row0;
-		k.depth = job.depth;
-		k.io = job.io;
+		k.depth = ln.depth;
+		k.io = ln.io;
 		k.n0 = ln.n0;
+		k.rows_hash = ln.rows_hash;
 		return k;
 	}
 
@@ -451,10 +457,10 @@ struct Render {
 	// (no host round trip between levels): the same streams and dependencies as the
 	// host-driven schedule: the chain on ln.stream, direct levels' shading on shade[L % 3]
 	// as soon as their k_closest is done, the deep levels in batches on shade[3] after the
-	// chain, then reductions and the output.  capture: recorded into a graph (the output
-	// pointers then come from ln.jobio_dev), with events of its own.
-	int issue_plan(Lane& ln, const Job& job, Plan& pl, bool capture) {
-		const int nlev = pl.n_levels, depth = job.depth;
+	// chain, then reductions and the output.  capture: recorded into a graph (with events
+	// of its own; the row table it reads is rewritten for every chunk).
+	int issue_plan(Lane& ln, Plan& pl, bool capture) {
+		const int nlev = pl.n_levels, depth = ln.depth;
 		int rc = RT_OK;
 		std::vector<hipEvent_t> tmp;
 		if (!capture && (rc = ensure_events(ln, nlev))) return rc;
@@ -471,9 +477,6 @@ struct Render {
 			if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string("planned launch: ") + hipGetErrorString(e));
 		};
 		int launches[3] = {0, 0, 0};
-		const int64_t W = job.W;
-		double* out = capture || !job.out_rgb_dev ? nullptr : job.out_rgb_dev + ln.r0 * W * 3;
-		uint8_t* out8 = capture || !job.out_rgb8_dev ? nullptr : job.out_rgb8_dev + ln.r0 * W * 3;
 		hipStream_t st = ln.stream;
 		std::vector<hipEvent_t> joins;
 		Plan scratch = pl;
@@ -523,8 +526,8 @@ struct Render {
 			step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1, ln.levels[l].lv,
 			                                ln.levels[l + 1].lv, st));
 		if (rc == RT_OK)
-			step(rtamd::launch_output(ln.n0, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, out, out8,
-			                          capture ? ln.jobio_dev : nullptr, job.io, s->stats, st));
+			step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
+			                          st));
 		for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
 		for (hipEvent_t e : tmp) (void)hipEventDestroy(e);
 		return rc;
@@ -532,9 +535,9 @@ struct Render {
 
 	// A plan for the chunk just traced host-driven (its shape: ln.fg, ln.n0, the job's
 	// depth; its levels: ln.level_n); with RTAMD_GRAPH=1 also captured into a hipGraph.
-	int build_plan(Lane& ln, const Job& job) {
+	int build_plan(Lane& ln) {
 		Plan pl;
-		pl.key = key_of(ln, job);
+		pl.key = key_of(ln);
 		pl.n_levels = static_cast<int>(ln.level_n.size());
 		pl.level_n = ln.level_n;
 		for (int L = 0; L < pl.n_levels; L++) pl.hits.push_back(ln.counts_host[2 * L]);
@@ -542,7 +545,7 @@ struct Render {
 		if (s->graphs == 1) {
 			hipGraph_t graph = nullptr;
 			HIP_TRY(hipStreamBeginCapture(ln.stream, hipStreamCaptureModeThreadLocal));
-			int rc = issue_plan(ln, job, pl, true);
+			int rc = issue_plan(ln, pl, true);
 			const hipError_t ec = hipStreamEndCapture(ln.stream, &graph);
 			if (rc == RT_OK && ec != hipSuccess)
 				rc = fail(RT_ERR_DEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
@@ -555,35 +558,69 @@ struct Render {
 		return RT_OK;
 	}
 
-	int start_chunk(Lane& ln, Job& job, int64_t r0, int64_t rows) {
-		const rt_render_params* p = job.p;
-		ln.job = &job;
+	// the chunk's row table: image row and output rows of every selected row of its pieces
+	int upload_rows(Lane& ln, const std::vector<Segment>& segs, int64_t n_rows) {
+		if (ln.rows_cap < n_rows) {
+			clear_plans(ln);  // graphs hold the table's address
+			if (ln.rows_dev) HIP_TRY(hipFree(ln.rows_dev));
+			if (ln.rows_pin) HIP_TRY(hipHostFree(ln.rows_pin));
+			ln.rows_dev = nullptr;
+			ln.rows_pin = nullptr;
+			ln.rows_cap = 0;
+			const int64_t cap = std::max<int64_t>(n_rows, 1024);
+			HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ln.rows_dev), cap * sizeof(rtamd::ChunkRow)));
+			HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.rows_pin), cap * sizeof(rtamd::ChunkRow),
+			                      hipHostMallocDefault));
+			ln.rows_cap = cap;
+		}
+		uint64_t h = 1469598103934665603ull;
+		int64_t q = 0;
+		for (const Segment& sg : segs) {
+			const Job& job = *sg.job;
+			const rt_render_params* p = job.p;
+			for (int64_t k = 0; k < sg.rows; k++, q++) {
+				const int64_t ord = sg.r0 + k;  // the job's selected-row ordinal: its output row
+				rtamd::ChunkRow& r = ln.rows_pin[q];
+				r.row = static_cast<int32_t>(p->row_begin + ord * p->row_step);
+				r.pad = 0;
+				r.out = job.out_rgb_dev ? job.out_rgb_dev + ord * job.W * 3 : nullptr;
+				r.out8 = job.out_rgb8_dev ? job.out_rgb8_dev + ord * job.W * 3 : nullptr;
+				h = (h ^ static_cast<uint32_t>(r.row)) * 1099511628211ull;
+			}
+		}
+		ln.rows_hash = h;
+		HIP_TRY(hipMemcpyAsync(ln.rows_dev, ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow), hipMemcpyHostToDevice,
+		                       ln.stream));
+		return RT_OK;
+	}
+
+	// a chunk: rows of one or several jobs of equal width, height, depth and io (render_jobs)
+	int start_chunk(Lane& ln, const std::vector<Segment>& segs) {
+		const Job& first = *segs.front().job;
+		int64_t n_rows = 0;
+		for (const Segment& sg : segs) n_rows += sg.rows;
+		ln.segs = segs;
+		ln.depth = first.depth;
+		ln.io = first.io;
+		ln.n0 = n_rows * first.W;
+		int rc = upload_rows(ln, segs, n_rows);
+		if (rc) return rc;
 		ln.fg = rtamd::FrameGeometry{};
-		ln.fg.width = p->width;
-		ln.fg.height = p->height;
-		ln.fg.row_begin = p->row_begin;
-		ln.fg.row_step = p->row_step;
-		ln.fg.chunk_row0 = static_cast<int32_t>(r0);
-		ln.fg.intersection_only = job.io;
-		ln.r0 = r0;
-		ln.n0 = rows * job.W;
+		ln.fg.width = first.p->width;
+		ln.fg.height = first.p->height;
+		ln.fg.intersection_only = first.io;
+		ln.fg.rows = ln.rows_dev;
 		ln.level = 0;
 		ln.level_n.assign(1, ln.n0);
 		ln.shaded.clear();
 		ln.deferred.clear();
 		ln.planned = nullptr;
-		if (Plan* pl = find_plan(ln, key_of(ln, job))) {
+		if (Plan* pl = find_plan(ln, key_of(ln))) {
 			if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
-			if (pl->exec) {  // graph replay: only the output record changes
-				const int64_t W = job.W;
-				ln.jobio_pin->out = job.out_rgb_dev ? job.out_rgb_dev + r0 * W * 3 : nullptr;
-				ln.jobio_pin->out8 = job.out_rgb8_dev ? job.out_rgb8_dev + r0 * W * 3 : nullptr;
-				HIP_TRY(hipMemcpyAsync(ln.jobio_dev, ln.jobio_pin, sizeof(rtamd::JobIO), hipMemcpyHostToDevice,
-				                       ln.stream));
+			if (pl->exec) {
 				HIP_TRY(hipGraphLaunch(pl->exec, ln.stream));
-			} else {
-				const int rc = issue_plan(ln, job, *pl, false);
-				if (rc) return rc;
+			} else if ((rc = issue_plan(ln, *pl, false))) {
+				return rc;
 			}
 			HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
 			ln.planned = pl;
@@ -591,9 +628,9 @@ struct Render {
 			return RT_OK;
 		}
 		ln.phase = Lane::TRACING;
-		int rc = ensure_level_record(s, ln, 0, ln.n0);
+		rc = ensure_level_record(s, ln, 0, ln.n0);
 		if (!rc) rc = launch_closest_level(ln, 0, ln.n0, nullptr);
-		if (!rc && job.depth >= 1) rc = launch_closest_level(ln, 1, 2 * ln.n0, ln.levels[0].lv.counts + 1);
+		if (!rc && ln.depth >= 1) rc = launch_closest_level(ln, 1, 2 * ln.n0, ln.levels[0].lv.counts + 1);
 		return rc;
 	}
 
@@ -602,8 +639,7 @@ struct Render {
 	// MathException is reported after the render (the reference aborts; the GPU merely
 	// finishes the chunk).
 	int on_counts(Lane& ln) {
-		const Job& job = *ln.job;
-		const int depth = job.depth;
+		const int depth = ln.depth;
 		const int L = ln.level;
 		const int64_t nh = ln.counts_host[2 * L], nn = ln.counts_host[2 * L + 1];
 		int rc;
@@ -633,10 +669,7 @@ struct Render {
 		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 1; l--)
 			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], nullptr, ln.levels[l].lv, ln.levels[l + 1].lv,
 			                                   ln.stream));
-		const int64_t W = job.W;
-		HIP_TRY(rtamd::launch_output(ln.n0, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
-		                             job.out_rgb_dev ? job.out_rgb_dev + ln.r0 * W * 3 : nullptr,
-		                             job.out_rgb8_dev ? job.out_rgb8_dev + ln.r0 * W * 3 : nullptr, nullptr, job.io,
+		HIP_TRY(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
 		                             s->stats, ln.stream));
 		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
 		ln.phase = Lane::FINISHING;
@@ -653,12 +686,12 @@ struct Render {
 			cnt.pixels += ln.n0;
 			ln.planned = nullptr;
 			ln.phase = Lane::IDLE;
-			ln.job = nullptr;
+			ln.segs.clear();
 			if (progress) progress->done += ln.n0;
 			return RT_OK;
 		}
-		if (s->graphs && !s->serial && !find_plan(ln, key_of(ln, *ln.job))) {
-			const int rc = build_plan(ln, *ln.job);
+		if (s->graphs && !s->serial && !find_plan(ln, key_of(ln))) {
+			const int rc = build_plan(ln);
 			if (rc) return rc;
 		}
 		for (int L = 0; L < static_cast<int>(ln.level_n.size()); L++) {
@@ -679,7 +712,7 @@ struct Render {
 		cnt.levels = std::max<int32_t>(cnt.levels, static_cast<int32_t>(ln.level_n.size()));
 		cnt.pixels += ln.n0;
 		ln.phase = Lane::IDLE;
-		ln.job = nullptr;
+		ln.segs.clear();
 		if (progress) progress->done += ln.n0;
 		return RT_OK;
 	}
@@ -945,6 +978,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);
 	if (const char* gr = std::getenv("RTAMD_GRAPH")) s->graphs = std::atoi(gr);
 	if (const char* pt = std::getenv("RTAMD_PLAN_TRUNCATE")) s->plan_truncate = std::atoi(pt);
+	if (const char* bc = std::getenv("RTAMD_BATCH_CHUNK")) s->batch_chunk_pixels = std::max<int64_t>(1, std::atoll(bc));
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
@@ -1037,7 +1071,7 @@ void reset_after_error(rt_scene* s) {
 	(void)hipDeviceSynchronize();
 	for (auto& ln : s->lanes) {
 		ln->phase = Lane::IDLE;
-		ln->job = nullptr;
+		ln->segs.clear();
 		ln->level = 0;
 		ln->level_n.clear();
 		ln->shaded.clear();
@@ -1067,7 +1101,6 @@ int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_coun
 		for (auto& ln : s->lanes) clear_plans(*ln);
 		const int graphs = s->graphs;
 		s->graphs = 0;
-		for (Job& j : jobs) j.next_row = 0;
 		if (progress) progress->done = 0;
 		rc = render_jobs_impl(s, jobs, caller, counters, progress);
 		s->graphs = graphs;
@@ -1096,28 +1129,52 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	// output buffers, completes before ours starts); the call returns when all is done
 	HIP_TRY(hipEventRecord(s->fork_event, caller));
 	for (size_t k = 0; k < n_lanes; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k]->stream, s->fork_event, 0));
-	for (Job& job : jobs) {
-		// chunks: at most 4 M pixels (bounds the level buffers); one image over several
-		// lanes is split so that every lane holds `chunks_per_lane` of its chunks
-		const rt_render_params* p = job.p;
-		const int64_t max_rows =
-		    std::max<int64_t>(1, (p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22) / job.W);
-		const int64_t want = (!batch && n_lanes > 1) ? static_cast<int64_t>(n_lanes) * s->chunks_per_lane : 1;
-		job.chunk_rows = std::min(max_rows, std::max<int64_t>(1, (job.n_rows + want - 1) / want));
-		job.next_row = 0;
+	// Pieces: every job's selected rows cut into pieces of at most its chunk size (4 M
+	// pixels by default: it bounds the level buffers); one image over several lanes is cut
+	// so that every lane holds `chunks_per_lane` of its pieces.  Consecutive pieces of
+	// different jobs with equal width, height, depth and io are packed into one chunk, up to
+	// batch_chunk_pixels: rows of several frames traced as one wavefront (a GPU's share of
+	// row-partitioned frames is a few rows of each frame).
+	std::vector<std::vector<Segment>> chunks;
+	{
+		std::vector<Segment> cur;
+		int64_t cur_px = 0, cur_limit = 0;
+		for (const Job& job : jobs) {
+			const rt_render_params* p = job.p;
+			const int64_t limit_px = p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22;
+			const int64_t max_rows = std::max<int64_t>(1, limit_px / job.W);
+			const int64_t want = (!batch && n_lanes > 1) ? static_cast<int64_t>(n_lanes) * s->chunks_per_lane : 1;
+			const int64_t piece = std::min(max_rows, std::max<int64_t>(1, (job.n_rows + want - 1) / want));
+			for (int64_t r0 = 0; r0 < job.n_rows; r0 += piece) {
+				const Segment sg{&job, r0, std::min(piece, job.n_rows - r0)};
+				const int64_t px = sg.rows * job.W;
+				bool fits = false;
+				if (!cur.empty()) {
+					const Job& f = *cur.front().job;
+					fits = cur.back().job != &job && f.p->width == p->width && f.p->height == p->height &&
+					       f.depth == job.depth && f.io == job.io &&
+					       cur_px + px <= std::min({cur_limit, limit_px, s->batch_chunk_pixels});
+				}
+				if (!fits && !cur.empty()) {
+					chunks.push_back(cur);
+					cur.clear();
+					cur_px = 0;
+				}
+				cur_limit = cur.empty() ? limit_px : std::min(cur_limit, limit_px);
+				cur.push_back(sg);
+				cur_px += px;
+			}
+		}
+		if (!cur.empty()) chunks.push_back(cur);
 	}
-	size_t next_job = 0;
+	size_t next_chunk = 0;
 	for (;;) {
 		bool busy = false;
 		for (size_t k = 0; k < n_lanes; k++) {
 			Lane& ln = *s->lanes[k];
 			if (ln.phase == Lane::IDLE) {
-				while (next_job < jobs.size() && jobs[next_job].next_row >= jobs[next_job].n_rows) next_job++;
-				if (next_job >= jobs.size()) continue;
-				Job& job = jobs[next_job];
-				const int64_t rows = std::min(job.chunk_rows, job.n_rows - job.next_row);
-				if ((rc = R.start_chunk(ln, job, job.next_row, rows))) return rc;
-				job.next_row += rows;
+				if (next_chunk >= chunks.size()) continue;
+				if ((rc = R.start_chunk(ln, chunks[next_chunk++]))) return rc;
 				busy = true;
 				continue;
 			}

@@ -46,11 +46,22 @@ struct RayLevel {
 	int64_t capacity;
 };
 
+// One row of a chunk: the image row it renders and where its pixels go.  A chunk holds
+// the selected rows of one frame or of several frames of the same width, height and depth
+// (rt_render_batch_device): small row selections, such as one GPU's share of
+// row-partitioned frames, are then traced as one full-size wavefront.
+struct ChunkRow {
+	int32_t row;       // image row r: Camera::calculateViewingRay's rowFrac = (r + 0.5) / H (scene.cpp:28)
+	int32_t pad;
+	double* out;       // this row's f64 pixels (W x 3), or null
+	uint8_t* out8;     // this row's RGB8 pixels, or null
+};
+
 struct FrameGeometry {
 	int32_t width, height;
-	int32_t row_begin, row_step;  // selected rows: row_begin + k*row_step
-	int32_t chunk_row0;           // first selected-row ordinal of this chunk
 	int32_t intersection_only;
+	int32_t pad;
+	const ChunkRow* rows;         // the chunk's rows (device), pixel i -> row i / width
 };
 
 // Device error word (first MathException code).  Ray and hit counts live per level
@@ -114,12 +125,7 @@ struct ShadeBatch {
 	const int32_t* nh_dev[kMaxBatch];
 };
 
-// Output pointers of a chunk read by k_output from device memory (a graph replays one
-// launch sequence for every frame; only this record changes)
-struct JobIO {
-	double* out;
-	uint8_t* out8;
-};
+
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
                          unsigned long long* stats, hipStream_t stream, int packet_mask);
 // ShadeBatch::fused may be set only when this holds (the wave-packet all-lights form)
@@ -131,10 +137,9 @@ hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const Sha
 hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,
                                hipStream_t stream);
 // lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output;
-// io_ptrs non-null: the output pointers are read from it (out_rgb / out_rgb8 ignored)
-hipError_t launch_output(int64_t n, const RayLevel& lvl0, const RayLevel* lvl1, double* out_rgb, uint8_t* out_rgb8,
-                         const JobIO* io_ptrs, int32_t intersection_only, unsigned long long* stats,
-                         hipStream_t stream);
+// pixels go to their rows' outputs (fg.rows)
+hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
+                         unsigned long long* stats, hipStream_t stream);
 // End of a render: summary[k] = sum over the shards of statistic k (max for ST_MAX_BITS),
 // summary[ST_COUNT] = the device error word; the shards and the error word are cleared for
 // the next render.

@@ -76,8 +76,7 @@ __device__ __forceinline__ void level_ray(const DeviceScene& S, const FrameGeome
                                           const LV& cur, V3& o, V3& d, bool& inside, DeviceCounters* ctr) {
 	if (level == 0) {
 		const int64_t q = div_small(i, fg.width);
-		const int64_t row_ord = fg.chunk_row0 + q;
-		const int r = fg.row_begin + (int)row_ord * fg.row_step;
+		const int r = fg.rows[q].row;
 		const int c = (int)(i - q * fg.width);
 		primary_ray(S.cam, r, c, fg.width, fg.height, o, d, ctr);
 		inside = false;
@@ -629,12 +628,18 @@ __device__ __forceinline__ uint8_t to_u8(double v) {
 
 // the image: level 0's colours, reduced with level 1 on the fly when `reduce` (the last
 // k_reduce fused into the output)
-__global__ void k_output(int64_t n, RayLevel lvl0, RayLevel lvl1, int32_t reduce, double* out, uint8_t* out8,
-                         const JobIO* io_ptrs, int32_t io, unsigned long long* stats) {
+__global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lvl1, int32_t reduce,
+                         unsigned long long* stats) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	if (io_ptrs) {
-		out = uniform_ptr(io_ptrs)->out;
-		out8 = uniform_ptr(io_ptrs)->out8;
+	const int32_t io = fg.intersection_only;
+	double* out = nullptr;
+	uint8_t* out8 = nullptr;
+	int64_t c = 0;
+	if (i < n) {  // pixel i: column c of the chunk's row q, written to that row's outputs
+		const int64_t q = div_small(i, fg.width);
+		c = i - q * fg.width;
+		out = fg.rows[q].out;
+		out8 = fg.rows[q].out8;
 	}
 	// level 0's counts were read back; clear them for the lane's next chunk
 	if (i == 0) lvl0.counts[0] = lvl0.counts[1] = 0;
@@ -648,14 +653,14 @@ __global__ void k_output(int64_t n, RayLevel lvl0, RayLevel lvl1, int32_t reduce
 			v[2] = lvl0.cb[i];
 		}
 		if (out) {
-			out[i * 3 + 0] = v[0];
-			out[i * 3 + 1] = v[1];
-			out[i * 3 + 2] = v[2];
+			out[c * 3 + 0] = v[0];
+			out[c * 3 + 1] = v[1];
+			out[c * 3 + 2] = v[2];
 		}
 		if (out8 && !io) {
-			out8[i * 3 + 0] = to_u8(v[0]);
-			out8[i * 3 + 1] = to_u8(v[1]);
-			out8[i * 3 + 2] = to_u8(v[2]);
+			out8[c * 3 + 0] = to_u8(v[0]);
+			out8[c * 3 + 1] = to_u8(v[1]);
+			out8[c * 3 + 2] = to_u8(v[2]);
 		}
 	}
 	if (io) {  // running max of maxCoeff over positive doubles (bit order == value order)
@@ -799,11 +804,11 @@ hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& 
 	return hipGetLastError();
 }
 
-hipError_t launch_output(int64_t n, const RayLevel& lvl0, const RayLevel* lvl1, double* out_rgb, uint8_t* out_rgb8,
-                         const JobIO* io_ptrs, int32_t io, unsigned long long* stats, hipStream_t stream) {
+hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
+                         unsigned long long* stats, hipStream_t stream) {
 	if (n <= 0) return hipSuccess;
-	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, lvl0, lvl1 ? *lvl1 : lvl0,
-	                   lvl1 ? 1 : 0, out_rgb, out_rgb8, io_ptrs, io, stats);
+	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, fg, lvl0, lvl1 ? *lvl1 : lvl0,
+	                   lvl1 ? 1 : 0, stats);
 	return hipGetLastError();
 }
 

@@ -241,3 +241,45 @@ def test_plan_miss_is_redone_exactly(gpu, oracle, scene, bdepth, io, graph, monk
         assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
         assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
     s.close()
+
+
+@pytest.mark.parametrize("pack", ["4194304", "20000", "1"])
+@pytest.mark.parametrize("graph", ["0", "2"])
+def test_multi_frame_chunks(gpu, oracle, pack, graph, monkeypatch):
+    """Chunks packed from rows of several frames (consecutive batch entries with equal width,
+    height and depth: one GPU's shares of row-partitioned frames, whole frames, chunked
+    frames) trace as one wavefront; every entry equals its own render, bit for bit, and the
+    summed counters equal the single renders' (RTAMD_BATCH_CHUNK bounds the packing)."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("RTAMD_BATCH_CHUNK", pack)
+    monkeypatch.setenv("RTAMD_GRAPH", graph)
+    scene = "excess_inputs/refraction3.rti"
+    w, h, bd = 70, 44, 7
+    want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bd)
+    s = gpu.load_scene(os.path.join(SCENES, scene))
+    jobs = [s.params(w, h, bd, False, r, h, 4) for r in range(4)] + [s.params(w, h, bd, False)] + \
+        [s.params(w, h, bd, False, 1, h, 2), s.params(w, h, bd, False, chunk_pixels=600)] + \
+        [s.params(w, h, 3, False, 0, h, 2), s.params(w, h, bd, False, 0, h, 3)]
+    rows = lambda p: len(range(p.row_begin, p.row_end, p.row_step))
+    for _ in range(3):  # host-driven, then planned chunks
+        outs = [torch.full((rows(p), w, 3), -1.0, dtype=torch.float64, device="cuda") for p in jobs]
+        out8 = [torch.zeros((rows(p), w, 3), dtype=torch.uint8, device="cuda") for p in jobs]
+        torch.cuda.synchronize()
+        st = s.render_batch_device(jobs, [o.data_ptr() for o in outs], [o.data_ptr() for o in out8])
+        for k, p in enumerate(jobs):
+            if p.bounce_depth != bd:
+                continue
+            ref = want[p.row_begin:p.row_end:p.row_step]
+            assert np.array_equal(outs[k].cpu().numpy().view(np.uint64), ref.view(np.uint64)), k
+            assert np.array_equal(out8[k].cpu().numpy(), gpu.to_rgb8(ref)), k
+    # counters: 3 whole frames at depth bd (4 quarter shares + 2 halves... = 1 + 1 + 1 + 1 frame
+    # of rows 0::3) and one half frame at depth 3 checked against single renders
+    single = [0, 0]
+    for p in jobs:
+        o = torch.empty((rows(p), w, 3), dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        one = s.render_device(p, o.data_ptr(), 0)
+        single[0] += one.trace_rays
+        single[1] += one.shadow_rays
+    assert [st.trace_rays, st.shadow_rays] == single
+    s.close()
