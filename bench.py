@@ -10,8 +10,9 @@ and equal to the reference's counts.  Inputs (the scene) are resident in HBM bef
 timed region; every frame is written as the reference's f64 RasterImage and as RGB8.
 
 Multi-GPU (torchrun, one rank per GPU, RCCL over xGMI), --mode partition (default): every
-frame is row-partitioned over the N ranks (row r -> rank r mod N, the reference's
-image-space decomposition of scene.cpp:13-48 spread over GPUs), each rank renders its rows
+frame is row-partitioned over the N ranks (8-row blocks interleaved: row r -> rank (r // 8)
+mod N, the reference's image-space decomposition of scene.cpp:13-48 spread over GPUs; a
+GPU's rows of all the step's frames are traced as shared wavefronts), each rank renders its rows
 of all frames of the step (pipelined, rt_render_batch_device) and every frame's RGB8 rows
 are gathered to rank 0 over RCCL.  The total work per step is fixed: "scaling": "strong".
 --mode replica: frame-parallel instead (each rank renders whole frames, gathered to rank 0;
@@ -64,7 +65,10 @@ def parse():
     ap.add_argument("--emulate-ranks", type=int, default=1,
                     help="development: on ONE GPU, render only rank 0's rows of an N-way partition (the per-GPU "
                          "work of an N-GPU run, to tune it without N GPUs); the line then reports that share")
-    ap.add_argument("--frames-per-step", type=int, default=16,
+    ap.add_argument("--row-block", type=int, default=8,
+                    help="partition granularity: blocks of this many rows interleaved over the ranks (8 = the "
+                         "8x8 ray tiles stay whole)")
+    ap.add_argument("--frames-per-step", type=int, default=32,
                     help="frames per step (partition: in total, every frame split over the ranks; "
                          "replica: per rank)")
     ap.add_argument("--sweep", default="C5_refraction3_4096_bd8,C4_airboat_sub_1920x1080",
@@ -276,12 +280,14 @@ def strong_scaling(a, world, rank, local, groups, dist, torch):
         s.upload()
         stream = torch.cuda.current_stream().cuda_stream
         rows_curve = []
+        blk = max(1, a.row_block)
         for n, grp in groups:
-            n_max = -(-H // n)
+            n_max = max(rd.n_rows(H, k, n, blk) for k in range(n))
             buf = torch.zeros((n_max, W, 3), dtype=torch.uint8, device="cuda")
             frame = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
             bufs = [torch.empty_like(buf) for _ in range(n)] if rank == 0 and n > 1 else None
-            prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rank, H, n) if rank < n else None
+            prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rank * blk, H, n, row_block=blk) \
+                if rank < n else None
             samples = []
             for rep in range(a.sweep_reps + 1):  # rep 0: warm-up (level buffers for this row count)
                 if world > 1:
@@ -295,7 +301,8 @@ def strong_scaling(a, world, rank, local, groups, dist, torch):
                     t_render = time.perf_counter() - t0
                     rays = st.rays
                     if n > 1:
-                        rd.gather_rows(buf, H, dst=0, out=frame, bufs=bufs, group=grp, group_size=n, group_rank=rank)
+                        rd.gather_rows(buf, H, dst=0, out=frame, bufs=bufs, group=grp, group_size=n, group_rank=rank,
+                                       block=blk)
                     elif rank == 0:
                         frame.copy_(buf)
                     torch.cuda.synchronize()
@@ -325,7 +332,8 @@ def strong_scaling(a, world, rank, local, groups, dist, torch):
                 r["speedup"] = round(base / r["ms"], 3)
                 r["efficiency"] = round(base / r["ms"] / r["n_gpus"], 3)
             out[cfg] = {"scene": scene_rel, "width": W, "height": H, "bounce_depth": kw["bdepth"],
-                        "partition": "rows interleaved (row r -> rank r mod n), RGB8 rows gathered to rank 0 over "
+                        "partition": f"{blk}-row blocks interleaved (row r -> rank (r // {blk}) mod n), RGB8 rows "
+                                     "gathered to rank 0 over "
                                      + ("RCCL" if dist.is_initialized() and dist.get_backend() == "nccl" else
                                         "the process group" if world > 1 else "(no exchange at n = 1)"),
                         "curve": rows_curve}
@@ -372,15 +380,17 @@ def main():
     partition = a.mode == "partition"
     # this rank's rows of every frame (partition) or whole frames (replica)
     ways = world if a.emulate_ranks <= 1 else a.emulate_ranks * world
-    rows = rd.rank_rows(H, rank, ways) if partition else (0, H, 1)
-    n_loc = len(range(*rows))
-    n_buf = -(-H // ways) if partition else H  # gather buffers: the longest rank's row count
+    blk = max(1, a.row_block)
+    rows = rd.rank_rows(H, rank, ways, block=blk) if partition else (0, H, 1, 1)
+    n_loc = rd.n_rows(H, rank, ways, blk) if partition else H
+    # gather buffers: the longest rank's row count
+    n_buf = max(rd.n_rows(H, k, ways, blk) for k in range(ways)) if partition else H
     outs = [torch.empty((n_buf, W, 3), dtype=torch.float64, device="cuda") for _ in range(B)]
     # RGB8 double-buffered: the gathers of step i (side stream) overlap the render of step i+1
     out8s = [[torch.zeros((n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(B)] for _ in range(2)]
     gathered = [None, None]
     comm = torch.cuda.Stream() if world > 1 else torch.cuda.current_stream()
-    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], *rows)
+    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rows[0], rows[1], rows[2], row_block=rows[3])
     stream = torch.cuda.current_stream().cuda_stream
     gbufs = [torch.empty((n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
         if rank == 0 and world > 1 else None
@@ -408,7 +418,8 @@ def main():
                 if partition and ways != world:  # emulated share: no assembly
                     pass
                 elif partition:  # frame f assembled on rank 0 from every rank's rows
-                    rd.gather_rows(out8s[k][f], H, dst=0, out=frames[f] if rank == 0 else None, bufs=gbufs)
+                    rd.gather_rows(out8s[k][f], H, dst=0, out=frames[f] if rank == 0 else None, bufs=gbufs,
+                                   block=blk)
                 elif world > 1:  # whole frames of every rank to rank 0
                     rd.gather_frames(out8s[k][f], dst=0, out=frames[f * world:(f + 1) * world] if rank == 0 else None)
                 else:
@@ -508,10 +519,11 @@ def main():
                        "rays_per_frame": int(rays / a.steps / fps),
                        "ms_per_frame": round(elapsed / a.steps / fps * 1e3, 3),
                        "frame_latency_ms": round(latency * 1e3, 3),
+                       "row_block": blk if partition else None,
                        "parallelism": (f"EMULATED rank share: rank 0's {n_loc} of {H} rows of an {ways}-way "
                                        f"partition, {fps} frames/step on 1 GPU (development measure, not a job)"
                                        if ways != world else
-                                       f"{fps} frames/step, each row-interleaved over {world} GPU(s) "
+                                       f"{fps} frames/step, each split into {blk}-row blocks interleaved over {world} GPU(s) "
                                        f"({n_loc} rows of {H} on rank 0), pipelined renders per GPU, "
                                        f"{'RCCL' if a.backend == 'nccl' else 'gloo (rehearsal)'} gather "
                                        "of every frame's RGB8 rows to rank 0" if partition and world > 1 else

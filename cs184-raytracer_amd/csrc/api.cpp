@@ -333,6 +333,12 @@ void lane_destroy(Lane& ln) {
 	if (ln.stream) (void)hipStreamDestroy(ln.stream);
 }
 
+// image row of the selected-row ordinal q (rt_render_params: blocks of row_block rows)
+int32_t selected_row(const rt_render_params* p, int64_t q) {
+	const int64_t B = std::max(1, p->row_block);
+	return static_cast<int32_t>(p->row_begin + (q / B) * p->row_step * B + q % B);
+}
+
 // The render of one rt_render_device / rt_render_batch_device call: chunks of rows of
 // its jobs handed to lanes, each lane a small state machine advanced by the host as its
 // events complete.
@@ -581,7 +587,7 @@ struct Render {
 			for (int64_t k = 0; k < sg.rows; k++, q++) {
 				const int64_t ord = sg.r0 + k;  // the job's selected-row ordinal: its output row
 				rtamd::ChunkRow& r = ln.rows_pin[q];
-				r.row = static_cast<int32_t>(p->row_begin + ord * p->row_step);
+				r.row = selected_row(p, ord);
 				r.pad = 0;
 				r.out = job.out_rgb_dev ? job.out_rgb_dev + ord * job.W * 3 : nullptr;
 				r.out8 = job.out_rgb8_dev ? job.out_rgb8_dev + ord * job.W * 3 : nullptr;
@@ -720,7 +726,9 @@ struct Render {
 
 int64_t selected_rows(const rt_render_params* p) {
 	if (p->row_step <= 0 || p->row_end <= p->row_begin) return 0;
-	return (p->row_end - p->row_begin + p->row_step - 1) / p->row_step;
+	const int64_t B = std::max(1, p->row_block), span = (int64_t)p->row_step * B, len = p->row_end - p->row_begin;
+	// whole periods of `span` rows hold B selected rows each; the last one min(B, rest)
+	return (len / span) * B + std::min<int64_t>(B, len % span);
 }
 
 constexpr int kMaxLanes = 8;
@@ -743,7 +751,8 @@ int check_params(const rt_scene* s, const rt_render_params* p) {
 	if (!s || !p) return fail(RT_ERR_ARG, "null scene or params");
 	if (p->width <= 0 || p->height <= 0) return fail(RT_ERR_ARG, "Width and/or height must be positive.");
 	if (p->bounce_depth < 0) return fail(RT_ERR_ARG, "Bounce depth must be non-negative.");
-	if (p->row_begin < 0 || p->row_end > p->height || p->row_step <= 0 || p->row_begin > p->row_end)
+	// (row_begin >= row_end selects no row: a rank past the last row block of a partition)
+	if (p->row_begin < 0 || p->row_end > p->height || p->row_step <= 0 || p->row_block < 0)
 		return fail(RT_ERR_ARG, "bad row selection");
 	return RT_OK;
 }
@@ -1308,6 +1317,7 @@ int ensure_staging(rt_scene* s, int64_t n_pixels, bool f64, bool u8) {
 }
 
 bool whole_image(const rt_render_params* p) { return p->row_begin == 0 && p->row_end == p->height && p->row_step == 1; }
+// (row_step 1 selects every row whatever row_block is)
 
 int render_batch(rt_scene* s, int n, const rt_render_params* params, double* const* out_rgb_dev,
                  uint8_t* const* out_rgb8_dev, void* stream_v, rt_counters* counters, Progress* progress) {

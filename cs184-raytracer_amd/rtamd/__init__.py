@@ -55,7 +55,8 @@ class ArgumentError(RTError, ValueError):
 class rt_render_params(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("bounce_depth", ctypes.c_int32),
                 ("intersection_only", ctypes.c_int32), ("row_begin", ctypes.c_int32), ("row_end", ctypes.c_int32),
-                ("row_step", ctypes.c_int32), ("chunk_pixels", ctypes.c_int32)]
+                ("row_step", ctypes.c_int32), ("chunk_pixels", ctypes.c_int32), ("row_block", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 class rt_counters(ctypes.Structure):
@@ -179,6 +180,24 @@ def lib() -> ctypes.CDLL:
     return L
 
 
+def _rows4(rows, height):
+    """(begin, end, step[, block]) row selection (rt_render_params); None = every row."""
+    if rows is None:
+        return 0, height, 1, 1
+    return (tuple(rows) + (1,))[:4]
+
+
+def selected_rows(begin: int, end: int, step: int, block: int = 1) -> List[int]:
+    """The image rows a row selection renders, in order (rt_render_params: blocks of
+    `block` rows, one block every step * block rows)."""
+    block = max(1, block)
+    return [r for r in range(begin, end) if ((r - begin) // block) % step == 0]
+
+
+def selected_count(begin: int, end: int, step: int, block: int = 1) -> int:
+    return len(selected_rows(begin, end, step, block))
+
+
 def _raise(rc: int, what: str = "") -> None:
     if rc == RT_OK:
         return
@@ -296,9 +315,10 @@ class Scene:
         return i
 
     def params(self, width: int, height: int, bounce_depth: int, intersection_only: bool, row_begin: int = 0,
-               row_end: Optional[int] = None, row_step: int = 1, chunk_pixels: int = 0) -> rt_render_params:
+               row_end: Optional[int] = None, row_step: int = 1, chunk_pixels: int = 0,
+               row_block: int = 1) -> rt_render_params:
         return rt_render_params(width, height, bounce_depth, int(bool(intersection_only)), row_begin,
-                                height if row_end is None else row_end, row_step, chunk_pixels)
+                                height if row_end is None else row_end, row_step, chunk_pixels, row_block, 0)
 
     def renderScene(self, output: Optional[np.ndarray] = None,
                     phandler: Optional[Callable[[int, int], None]] = None, options: Optional[Options] = None,
@@ -306,18 +326,19 @@ class Scene:
         """Scene::renderScene (scene.cpp:10-59).
 
         ``output`` is the RasterImage: float64 array of shape (H, W, 3), caller-owned (allocated
-        here from ``options`` when None).  ``rows = (begin, end, step)`` renders a row-interleaved
-        subset into an (n_rows, W, 3) array (multi-GPU partition).
+        here from ``options`` when None).  ``rows = (begin, end, step[, block])`` renders a
+        row-interleaved subset (blocks of ``block`` rows) into an (n_rows, W, 3) array (multi-GPU
+        partition).
         """
         o = options or programOptions
         W, H = o.renderWidth_, o.renderHeight_
-        rb, re_, rs = rows if rows is not None else (0, H, 1)
-        n_rows = max(0, -(-(re_ - rb) // rs))
+        rb, re_, rs, blk = _rows4(rows, H)
+        n_rows = selected_count(rb, re_, rs, blk)
         if output is None:
             output = np.empty((n_rows, W, 3), dtype=np.float64)
         if output.dtype != np.float64 or output.shape != (n_rows, W, 3) or not output.flags.c_contiguous:
             raise ArgumentError(f"output must be a C-contiguous float64 array of shape {(n_rows, W, 3)}")
-        prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels)
+        prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels, blk)
         cb = PROGRESS_FN((lambda c, t, u: phandler(c, t)) if phandler else (lambda c, t, u: None))
         cnt = rt_counters()
         _raise(lib().rt_render(self.handle, ctypes.byref(prm), output.ctypes.data_as(ctypes.c_void_p), cb, None,
@@ -331,10 +352,10 @@ class Scene:
         returns a uint8 (n_rows, W, 3) array."""
         o = options or programOptions
         W, H = o.renderWidth_, o.renderHeight_
-        rb, re_, rs = rows if rows is not None else (0, H, 1)
-        n_rows = max(0, -(-(re_ - rb) // rs))
+        rb, re_, rs, blk = _rows4(rows, H)
+        n_rows = selected_count(rb, re_, rs, blk)
         out = np.empty((n_rows, W, 3), dtype=np.uint8)
-        prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels)
+        prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels, blk)
         cb = PROGRESS_FN((lambda c, t, u: phandler(c, t)) if phandler else (lambda c, t, u: None))
         cnt = rt_counters()
         _raise(lib().rt_render_rgb8(self.handle, ctypes.byref(prm), out.ctypes.data_as(ctypes.c_void_p), cb, None,

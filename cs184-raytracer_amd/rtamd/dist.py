@@ -19,14 +19,21 @@ import torch
 import torch.distributed as dist
 
 
-def rank_rows(height: int, rank: int, world: int, shift: int = 0) -> Tuple[int, int, int]:
-    """(row_begin, row_end, row_step) of this rank's rows; with `shift`, rank r holds the
-    rows of residue (r + shift) mod world (frame `shift` of a rotated batch)."""
-    return (rank + shift) % world, height, world
+def rank_rows(height: int, rank: int, world: int, shift: int = 0, block: int = 1) -> Tuple[int, int, int, int]:
+    """(row_begin, row_end, row_step, row_block) of this rank's rows: blocks of `block` rows
+    interleaved over the ranks (row r -> rank (r // block) mod world); with `shift`, rank r
+    holds the blocks of residue (r + shift) mod world (frame `shift` of a rotated batch)."""
+    return ((rank + shift) % world) * block, height, world, block
 
 
-def n_rows(height: int, rank: int, world: int) -> int:
-    return len(range(rank, height, world))
+def rows_of(height: int, rank: int, world: int, block: int = 1):
+    """The image rows of rank `rank`, in the order it renders them."""
+    b = max(1, block)
+    return [r for r in range(rank * b, height) if ((r - rank * b) // b) % world == 0]
+
+
+def n_rows(height: int, rank: int, world: int, block: int = 1) -> int:
+    return len(rows_of(height, rank, world, block))
 
 
 def global_max(value: float, device: torch.device) -> float:
@@ -42,12 +49,12 @@ def global_max(value: float, device: torch.device) -> float:
 def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
                 out: Optional[torch.Tensor] = None, bufs: Optional[list] = None, shift: int = 0,
                 group=None, group_size: Optional[int] = None,
-                group_rank: Optional[int] = None) -> Optional[torch.Tensor]:
+                group_rank: Optional[int] = None, block: int = 1) -> Optional[torch.Tensor]:
     """Gathers every rank's interleaved rows (n_local, W, C) into a (H, W, C) frame on `dst`
-    (rank r holds rows (r + shift) mod world, see rank_rows).  `local` may be longer than the
-    rank's row count (a buffer of the longest rank's rows): the extra rows are ignored.
-    With `group` (a sub-communicator of ranks 0 .. group_size - 1), world = group_size and
-    the rank is group_rank; `dst` is a global rank inside the group."""
+    (rank r holds the row blocks of residue (r + shift) mod world, see rank_rows).  `local`
+    may be longer than the rank's row count (a buffer of the longest rank's rows): the extra
+    rows are ignored.  With `group` (a sub-communicator of ranks 0 .. group_size - 1),
+    world = group_size and the rank is group_rank; `dst` is a global rank inside the group."""
     world = group_size if group is not None else (dist.get_world_size() if dist.is_initialized() else 1)
     rank = group_rank if group is not None else (dist.get_rank() if dist.is_initialized() else 0)
     if world == 1:
@@ -56,7 +63,7 @@ def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
             return rows.clone()
         out.copy_(rows)
         return out
-    n_max = -(-height // world)
+    n_max = max(n_rows(height, k, world, block) for k in range(world))
     if not local.is_contiguous():
         local = local.contiguous()
     if local.shape[0] != n_max:
@@ -75,10 +82,24 @@ def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
             out = torch.empty((height,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
         for r in range(world):
             k = (r + shift) % world
-            out[k::world] = bufs[r][: n_rows(height, k, world)].to(out.device)
+            if block <= 1:
+                out[k::world] = bufs[r][: n_rows(height, k, world)].to(out.device)
+            else:
+                idx = _row_index(height, k, world, block, out.device)
+                out[idx] = bufs[r][: idx.numel()].to(out.device)
         return out
     dist.gather(local, None, dst=dst, group=group)
     return None
+
+
+_ROW_INDEX = {}
+
+
+def _row_index(height, rank, world, block, device):
+    key = (height, rank, world, block, str(device))
+    if key not in _ROW_INDEX:
+        _ROW_INDEX[key] = torch.tensor(rows_of(height, rank, world, block), dtype=torch.long, device=device)
+    return _ROW_INDEX[key]
 
 
 def gather_frames(frame: torch.Tensor, dst: int = 0, out: Optional[list] = None) -> Optional[list]:
@@ -120,16 +141,17 @@ def gather_batch(full: torch.Tensor, height: int, dst: int = 0, frames: Optional
     return outs if rank == dst else None
 
 
-def render_frame(render_rows: Callable[[Tuple[int, int, int]], Tuple[torch.Tensor, float]], height: int,
-                 intersection_only: bool, device: torch.device, dst: int = 0) -> Optional[torch.Tensor]:
+def render_frame(render_rows: Callable[[Tuple[int, int, int, int]], Tuple[torch.Tensor, float]], height: int,
+                 intersection_only: bool, device: torch.device, dst: int = 0, block: int = 1) -> Optional[torch.Tensor]:
     """Distributed Scene::renderScene: returns the (H, W, 3) float64 frame on `dst`.
 
-    render_rows(rows) renders this rank's rows and returns (float64 (n_local, W, 3), local max).
+    render_rows(rows) renders this rank's rows (begin, end, step, block) and returns
+    (float64 (n_local, W, 3), local max).
     """
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
-    img, local_max = render_rows(rank_rows(height, rank, world))
+    img, local_max = render_rows(rank_rows(height, rank, world, block=block))
     if intersection_only:
         m = global_max(max(local_max, 2.2250738585072014e-308), device)  # max init DBL_MIN (scene.cpp:51)
         img.mul_(1.0 / m)  # Color3d /= scalar multiplies by the reciprocal
-    return gather_rows(img, height, dst)
+    return gather_rows(img, height, dst, block=block)

@@ -160,11 +160,15 @@ typedef struct rt_render_params {
 	int32_t width, height;        /* -w / -h (options.h:13-14)                             */
 	int32_t bounce_depth;         /* --bdepth (options.h:15), >= 0                         */
 	int32_t intersection_only;    /* --intersection-only (options.h:16)                    */
-	/* Rows rendered: row_begin, row_begin+row_step, ... < row_end (row-interleaved
-	 * multi-GPU partition).  {0, height, 1} renders the whole image. */
+	/* Rows rendered, in this order: blocks of row_block consecutive rows (0 or 1: single
+	 * rows) starting at row_begin, row_begin + row_step*row_block, ... below row_end.  The
+	 * multi-GPU partition gives rank k of N {k*B, H, N} with B = row_block: row r goes to
+	 * rank (r / B) mod N.  {0, height, 1} renders the whole image. */
 	int32_t row_begin, row_end, row_step;
 	/* Pixels per wavefront pass (bounds queue memory); 0 = automatic. */
 	int32_t chunk_pixels;
+	int32_t row_block;            /* see row_begin; 0 = 1 */
+	int32_t reserved;
 } rt_render_params;
 
 typedef struct rt_counters {
@@ -194,7 +198,7 @@ typedef struct rt_counters {
 } rt_counters;
 
 /* Scene::renderScene into a caller-owned host buffer of n_rows*W*3 doubles
- * (n_rows = rows selected by row_begin/row_end/row_step, in that order).
+ * (n_rows = rows selected by row_begin/row_end/row_step/row_block, in that order).
  * With intersection_only and the whole image selected, the output is normalised by
  * the global maximum exactly as scene.cpp:50-58; otherwise the raw 1/d^2 values are
  * returned with counters->intersection_max for the caller's global reduction. */

@@ -22,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, scene, w, h, bdepth, io, q):
+def _worker(rank, world, port, scene, w, h, bdepth, io, q, block=1):
     import torch.distributed as dist
     import pyoracle
     from rtamd import dist as rd
@@ -30,27 +30,34 @@ def _worker(rank, world, port, scene, w, h, bdepth, io, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         def render_rows(rows):
-            img, _ = pyoracle.render(scene, w, h, bdepth=bdepth, intersection_only=io, threads=2, rows=rows)
+            begin, end, step, block = rows
+            if block == 1:
+                img, _ = pyoracle.render(scene, w, h, bdepth=bdepth, intersection_only=io, threads=2,
+                                         rows=(begin, end, step))
+            else:  # row blocks: the oracle's full image, this rank's rows
+                full, _ = pyoracle.render(scene, w, h, bdepth=bdepth, intersection_only=io, threads=2)
+                img = np.ascontiguousarray(full[rd.rows_of(h, begin // block, step, block)])
             local_max = float(np.nanmax(img)) if img.size else 0.0
             return torch.from_numpy(img), local_max
-        frame = rd.render_frame(render_rows, h, io, torch.device("cpu"))
+        frame = rd.render_frame(render_rows, h, io, torch.device("cpu"), block=block)
         if rank == 0:
             q.put(frame.numpy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scene,io", [("excess_inputs/refraction3.rti", False), ("inputs/input-02.rti", True),
-                                      ("inputs/input-09.rti", False)])
+@pytest.mark.parametrize("scene,io,block", [("excess_inputs/refraction3.rti", False, 1), ("inputs/input-02.rti", True, 1),
+                                            ("inputs/input-09.rti", False, 1), ("excess_inputs/refraction3.rti", False, 4),
+                                            ("inputs/input-02.rti", True, 3)])
 @pytest.mark.parametrize("world", [2, 3])
-def test_partitioned_frame_equals_single_render(oracle, scene, io, world):
+def test_partitioned_frame_equals_single_render(oracle, scene, io, block, world):
     w, h, bdepth = 33, 23, 4
     path = os.path.join(SCENES, scene)
     want, _ = oracle.render(path, w, h, bdepth=bdepth, intersection_only=io)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, path, w, h, bdepth, io, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, path, w, h, bdepth, io, q, block)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)

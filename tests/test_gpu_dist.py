@@ -26,7 +26,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, scene, w, h, bdepth, io, q):
+def _worker(rank, world, port, scene, w, h, bdepth, io, q, block):
     import torch
     import torch.distributed as dist
     import rtamd
@@ -38,21 +38,21 @@ def _worker(rank, world, port, scene, w, h, bdepth, io, q):
         s = rtamd.load_scene(scene)
 
         def render_rows(rows):
-            n = len(range(*rows))
+            n = rtamd.selected_count(*rows)
             out = torch.empty((n, w, 3), dtype=torch.float64, device="cuda")
-            st = s.render_device(s.params(w, h, bdepth, io, *rows), out.data_ptr(), 0,
-                                 torch.cuda.current_stream().cuda_stream)
+            st = s.render_device(s.params(w, h, bdepth, io, rows[0], rows[1], rows[2], row_block=rows[3]),
+                                 out.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
             return out, st.intersection_max
-        frame = rd.render_frame(render_rows, h, io, torch.device("cuda"))
+        frame = rd.render_frame(render_rows, h, io, torch.device("cuda"), block=block)
         # RGB8 rows (bench.py's partition step): rendered on the device, gathered to rank 0
-        rows = rd.rank_rows(h, rank, world)
-        n_buf = -(-h // world)
+        rows = rd.rank_rows(h, rank, world, block=block)
+        n_buf = max(rd.n_rows(h, k, world, block) for k in range(world))
         out8 = torch.zeros((n_buf, w, 3), dtype=torch.uint8, device="cuda")
         if not io:
-            s.render_device(s.params(w, h, bdepth, io, *rows), 0, out8.data_ptr(),
-                            torch.cuda.current_stream().cuda_stream)
+            s.render_device(s.params(w, h, bdepth, io, rows[0], rows[1], rows[2], row_block=rows[3]), 0,
+                            out8.data_ptr(), torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
-        frame8 = rd.gather_rows(out8, h, dst=0)
+        frame8 = rd.gather_rows(out8, h, dst=0, block=block)
         if rank == 0:
             q.put((frame.cpu().numpy(), None if io else frame8.cpu().numpy()))
         s.close()
@@ -60,9 +60,12 @@ def _worker(rank, world, port, scene, w, h, bdepth, io, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("scene,opt", [("excess_inputs/bunny.rti", "w64h48"), ("excess_inputs/refraction3.rti", "w50h30_bd12"),
-                                       ("inputs/input-02.rti", "w31h17_io"), ("inputs/input-09.rti", "w37h23_bd2")])
-def test_two_ranks_hip_partition_matches_reference(gpu, golden, scene, opt):
+@pytest.mark.parametrize("scene,opt,block", [("excess_inputs/bunny.rti", "w64h48", 1),
+                                             ("excess_inputs/refraction3.rti", "w50h30_bd12", 1),
+                                             ("inputs/input-02.rti", "w31h17_io", 1), ("inputs/input-09.rti", "w37h23_bd2", 1),
+                                             ("excess_inputs/bunny.rti", "w64h48", 8),
+                                             ("inputs/input-02.rti", "w31h17_io", 4)])
+def test_two_ranks_hip_partition_matches_reference(gpu, golden, scene, opt, block):
     import torch.multiprocessing as mp
     name, w, h, flags = next(o for o in OPTION_SETS if o[0] == opt)
     kw = option_kwargs(flags)
@@ -71,7 +74,7 @@ def test_two_ranks_hip_partition_matches_reference(gpu, golden, scene, opt):
     q = ctx.Queue()
     port = _free_port()
     path = os.path.join(SCENES, scene)
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, w, h, kw["bdepth"], kw["intersection_only"], q))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, path, w, h, kw["bdepth"], kw["intersection_only"], q, block))
              for r in range(2)]
     for p in procs:
         p.start()
