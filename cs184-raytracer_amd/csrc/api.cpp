@@ -46,6 +46,11 @@ const char* device_error_text(int code) {  // MathException what() (rtbase.h:14-
 
 }  // namespace
 
+namespace rtamd {
+// rt_last_error() text for the calling thread (librtamd_multi reports through it)
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace rtamd
+
 struct rt_builder {
 	rtamd::Scene scene;
 	// rt_builder_get_desc views (rebuilt on every call)
@@ -1428,6 +1433,14 @@ int rt_normalize_device(rt_scene* s, double* rgb_dev, int64_t n_pixels, double m
 	HIP_TRY(rtamd::launch_normalize(n_pixels * 3, rgb_dev, max_value, out_rgb8_dev, st));
 	HIP_TRY(hipStreamSynchronize(st));
 	return RT_OK;
+}
+
+void rt_partition_row(int64_t row, int n_devices, int row_block, int* device, int64_t* local_row) {
+	int d = 0;
+	int64_t l = 0;
+	rtamd::partition_row(row, n_devices < 1 ? 1 : n_devices, row_block, &d, &l);
+	if (device) *device = d;
+	if (local_row) *local_row = l;
 }
 
 int rt_write_png(const char* path, const uint8_t* rgb, int width, int height) {

@@ -1,7 +1,9 @@
 // rtamd — drop-in replacement for the reference's `as2` executable (main.cpp:40-85,
 // options.cpp:7-90): same flags (-o/--output, -t/--threads, -w/--width, -h/--height,
 // --bdepth, --intersection-only, positional .rti files), same messages and exit codes,
-// byte-identical PNG.  Adds --device N (HIP device) and --dump-raw FILE (f64 image).
+// byte-identical PNG.  Adds --device N (HIP device), --dump-raw FILE (f64 image) and
+// --gpus N (devices --device .. --device+N-1 of this node, rows in --row-block blocks
+// interleaved over them, gathered over RCCL: include/rtamd_multi.h).
 // The render itself runs on the GPU through the C-ABI (include/rtamd.h).
 #include <getopt.h>
 #include <signal.h>
@@ -14,6 +16,7 @@
 #include <string>
 #include <vector>
 #include "../../include/rtamd.h"
+#include "../../include/rtamd_multi.h"
 
 namespace {
 
@@ -21,10 +24,11 @@ struct Options {  // options.h:10-16 defaults
 	std::vector<std::string> inputs;
 	std::string output, dump_raw;
 	int threads = 1, width = 500, height = 500, bdepth = 10, device = 0;
+	int gpus = 0, row_block = 8;  // gpus 0: the single-device path
 	bool intersection_only = false;
 };
 
-enum { OPT_HELP = 0, OPT_BDEPTH = 256, OPT_IO, OPT_DEVICE, OPT_DUMP };
+enum { OPT_HELP = 0, OPT_BDEPTH = 256, OPT_IO, OPT_DEVICE, OPT_DUMP, OPT_GPUS, OPT_ROW_BLOCK };
 
 bool parse_int(const char* s, int& out) {
 	try {
@@ -41,6 +45,7 @@ bool parse_command_line(int argc, char** argv, Options& o) {  // options.cpp:18-
 	                                     {"height", 1, nullptr, 'h'},        {"bdepth", 1, nullptr, OPT_BDEPTH},
 	                                     {"intersection-only", 0, nullptr, OPT_IO},
 	                                     {"device", 1, nullptr, OPT_DEVICE}, {"dump-raw", 1, nullptr, OPT_DUMP},
+	                                     {"gpus", 1, nullptr, OPT_GPUS},     {"row-block", 1, nullptr, OPT_ROW_BLOCK},
 	                                     {nullptr, 0, nullptr, 0}};
 	int c;
 	while ((c = getopt_long(argc, argv, "t:w:h:o:", opts, nullptr)) != -1) {
@@ -84,6 +89,18 @@ bool parse_command_line(int argc, char** argv, Options& o) {  // options.cpp:18-
 			case OPT_DEVICE:
 				if (!parse_int(optarg, o.device) || o.device < 0) {
 					std::cerr << "Error: Device index is invalid." << std::endl;
+					return false;
+				}
+				break;
+			case OPT_GPUS:
+				if (!parse_int(optarg, o.gpus) || o.gpus < 1) {
+					std::cerr << "Error: GPU count is invalid." << std::endl;
+					return false;
+				}
+				break;
+			case OPT_ROW_BLOCK:
+				if (!parse_int(optarg, o.row_block) || o.row_block < 1) {
+					std::cerr << "Error: Row block is invalid." << std::endl;
 					return false;
 				}
 				break;
@@ -151,7 +168,15 @@ int main(int argc, char** argv) {
 		return 1;
 	}
 	rt_scene* scene = nullptr;
-	if (rt_scene_create(b, o.device, &scene)) {
+	rt_multi* multi = nullptr;
+	if (o.gpus > 0) {
+		std::vector<int> devices;
+		for (int k = 0; k < o.gpus; k++) devices.push_back(o.device + k);
+		if (rt_multi_create(b, o.gpus, devices.data(), o.row_block, &multi)) {
+			std::cerr << "Error: " << rt_last_error() << std::endl;
+			return 1;
+		}
+	} else if (rt_scene_create(b, o.device, &scene)) {
 		std::cerr << "Error: " << rt_last_error() << std::endl;
 		return 1;
 	}
@@ -169,8 +194,10 @@ int main(int argc, char** argv) {
 	std::vector<double> img(o.dump_raw.empty() ? 0 : n);
 	std::vector<uint8_t> rgb(n);
 	set_alarm(true);
-	int rc = img.empty() ? rt_render_rgb8(scene, &p, rgb.data(), update_progress, nullptr, nullptr)
-	                     : rt_render(scene, &p, img.data(), update_progress, nullptr, nullptr);
+	int rc = multi ? rt_multi_render(multi, &p, img.empty() ? nullptr : img.data(), rgb.data(), update_progress,
+	                                 nullptr, nullptr)
+	         : img.empty() ? rt_render_rgb8(scene, &p, rgb.data(), update_progress, nullptr, nullptr)
+	                       : rt_render(scene, &p, img.data(), update_progress, nullptr, nullptr);
 	set_alarm(false);
 	if (rc == RT_ERR_MATH) {
 		std::cerr << "terminate called after throwing an instance of 'MathException'\n  what():  " << rt_last_error()
@@ -187,13 +214,14 @@ int main(int argc, char** argv) {
 			std::fwrite(img.data(), sizeof(double), img.size(), f);
 			std::fclose(f);
 		}
-		rt_to_rgb8(img.data(), static_cast<int64_t>(o.width) * o.height, rgb.data());
+		if (!multi) rt_to_rgb8(img.data(), static_cast<int64_t>(o.width) * o.height, rgb.data());
 	}
 	if (rt_write_png(o.output.c_str(), rgb.data(), o.width, o.height)) {
 		std::cerr << "Error: " << rt_last_error() << std::endl;
 		return 1;
 	}
-	rt_scene_destroy(scene);
+	if (scene) rt_scene_destroy(scene);
+	if (multi) rt_multi_destroy(multi);
 	rt_builder_destroy(b);
 	return 0;
 }

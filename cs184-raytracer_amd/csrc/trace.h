@@ -64,6 +64,23 @@ struct FrameGeometry {
 	const ChunkRow* rows;         // the chunk's rows (device), pixel i -> row i / width
 };
 
+// Row partition over devices (rt_partition_row): blocks of B rows interleaved over n
+__host__ __device__ inline void partition_row(int64_t row, int n, int B, int* dev, int64_t* local) {
+	B = B < 1 ? 1 : B;
+	const int64_t blk = row / B;
+	*dev = static_cast<int>(blk % n);
+	*local = (blk / n) * B + row % B;
+}
+
+// Multi-GPU assembly on the first device: image row r (row_bytes each) comes from device
+// partition_row(r)'s buffer src[dev] at its local row
+constexpr int kMaxGpus = 16;
+struct RowSources {
+	const uint8_t* src[kMaxGpus];
+};
+hipError_t launch_deinterleave(uint8_t* dst, const RowSources& s, int n, int block, int64_t height, int64_t row_bytes,
+                               hipStream_t stream);
+
 // Device error word (first MathException code).  Ray and hit counts live per level
 // (RayLevel::counts) so that levels in flight on different streams never share one.
 struct DeviceCounters {

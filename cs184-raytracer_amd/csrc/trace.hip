@@ -735,6 +735,20 @@ __global__ void k_stream_read(const T* __restrict__ p, int64_t n, unsigned long 
 	if (acc == 0x7fffffffffffffffull) sink[0] = acc;  // keeps the loads; never true for the zeroed buffer
 }
 
+// multi-GPU image assembly on the first device: one thread per byte of the image, each
+// row copied from its owner's buffer (partition_row)
+__global__ void k_deinterleave(uint8_t* dst, RowSources s, int n, int block, int64_t height, int64_t row_bytes) {
+	const int64_t total = height * row_bytes;
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+		const int64_t r = i / row_bytes, b = i - r * row_bytes;
+		int dev;
+		int64_t local;
+		partition_row(r, n, block, &dev, &local);
+		dst[i] = s.src[dev][local * row_bytes + b];
+	}
+}
+
 inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 // grid of the stride loops: 8 blocks (16 waves) per CU, 4 waves per SIMD
 constexpr int64_t kStrideBlocks = 256 * 8;
@@ -845,6 +859,15 @@ hipError_t launch_stream_read(const void* buf, int64_t bytes, int width, unsigne
 		case 8: hipLaunchKernelGGL(k_stream_read<uint64_t>, dim3(grid), dim3(256), 0, stream, (const uint64_t*)buf, bytes / 8, sink); break;
 		default: hipLaunchKernelGGL(k_stream_read<uint4>, dim3(grid), dim3(256), 0, stream, (const uint4*)buf, bytes / 16, sink); break;
 	}
+	return hipGetLastError();
+}
+
+hipError_t launch_deinterleave(uint8_t* dst, const RowSources& s, int n, int block, int64_t height, int64_t row_bytes,
+                               hipStream_t stream) {
+	const int64_t total = height * row_bytes;
+	if (total <= 0) return hipSuccess;
+	hipLaunchKernelGGL(k_deinterleave, dim3((unsigned)std::min<int64_t>(grid_for(total, 256), 8192)), dim3(256), 0,
+	                   stream, dst, s, n, block, height, row_bytes);
 	return hipGetLastError();
 }
 

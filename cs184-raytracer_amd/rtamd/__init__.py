@@ -162,6 +162,7 @@ def lib() -> ctypes.CDLL:
         "rt_scene_create_desc": (i32, [ctypes.POINTER(rt_scene_desc), i32, ctypes.POINTER(vp)]),
         "rt_debug_builder_digest": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
         "rt_debug_fail_after": (i32, [vp, i32]),
+        "rt_partition_row": (None, [i64, i32, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]),
         "rt_render_batch_device": (i32, [vp, i32, ctypes.POINTER(rt_render_params), ctypes.POINTER(vp),
                                          ctypes.POINTER(vp), vp, ctypes.POINTER(rt_counters)]),
         "rt_normalize_device": (i32, [vp, vp, i64, dbl, vp, vp]),
@@ -452,6 +453,13 @@ class PNGWriter:
         rgb = np.ascontiguousarray(rgb)
         h, w = rgb.shape[0], rgb.shape[1]
         _raise(lib().rt_write_png(os.fsencode(self.filename), rgb.ctypes.data_as(ctypes.c_void_p), w, h))
+
+
+def partition_row(row: int, n_devices: int, row_block: int):
+    """rt_partition_row: (device, local row) of image row `row` in the multi-GPU partition."""
+    d, l = ctypes.c_int(), ctypes.c_int64()
+    lib().rt_partition_row(row, n_devices, row_block, ctypes.byref(d), ctypes.byref(l))
+    return d.value, l.value
 
 
 def device_count() -> int:

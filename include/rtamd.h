@@ -234,6 +234,12 @@ int rt_render_batch_device(rt_scene* s, int n, const rt_render_params* params,
 int rt_normalize_device(rt_scene* s, double* rgb_dev, int64_t n_pixels, double max_value,
                         uint8_t* out_rgb8_dev, void* stream);
 
+/* The multi-GPU row partition (rtamd_multi.h, rtamd/dist.py): with blocks of row_block
+ * rows interleaved over n_devices, image row `row` is rendered by device *device as its
+ * *local_row-th selected row, i.e. by rt_render_params {device * row_block, H, n_devices,
+ * row_block} (the reference's block dispenser, scene.cpp:13-48, at GPU granularity). */
+void rt_partition_row(int64_t row, int n_devices, int row_block, int* device, int64_t* local_row);
+
 /* ---------------------------------------------------------------- output */
 /* writers.cpp:4-9: clamp to [0,1], *255, truncate (NaN -> 0). */
 void rt_to_rgb8(const double* rgb, int64_t n_pixels, uint8_t* out);

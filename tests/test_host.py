@@ -28,6 +28,33 @@ def test_library_exports_every_declared_function(rt):
         assert hasattr(rt.lib(), n), f"{n} declared in include/rtamd.h but not exported"
 
 
+def test_multi_library_exports_every_declared_function(rt):
+    """librtamd_multi.so (RCCL multi-GPU render) exports include/rtamd_multi.h; loading it
+    needs no GPU."""
+    import ctypes
+    text = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "rtamd_multi.h")).read(), flags=re.S)
+    names = sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(rt_multi\w+)\s*\(", text, flags=re.M)))
+    assert len(names) == 5
+    L = ctypes.CDLL(os.path.join(REPO, "cs184-raytracer_amd", "rtamd", "librtamd_multi.so"))
+    for n in names:
+        assert hasattr(L, n), n
+
+
+@pytest.mark.parametrize("n,block", [(1, 8), (2, 8), (3, 8), (8, 8), (4, 1), (3, 5), (16, 16)])
+def test_partition_row_matches_dist(rt, n, block):
+    """The multi-GPU de-interleave map (rt_partition_row, k_deinterleave's index math) is the
+    inverse of every device's row selection (rtamd.dist.rows_of / rt_render_params)."""
+    from rtamd import dist as rd
+    H = 1080
+    owner = {}
+    for d in range(n):
+        for k, r in enumerate(rd.rows_of(H, d, n, block)):
+            owner[r] = (d, k)
+    assert sorted(owner) == list(range(H))
+    for r in range(H):
+        assert rt.partition_row(r, n, block) == owner[r]
+
+
 @pytest.mark.parametrize("png", sorted(SHIPPED))
 def test_png_writer_is_byte_identical_to_libpng(rt, tmp_path, png):
     from PIL import Image
@@ -93,6 +120,7 @@ def test_pow_restatement_matches_libm(tmp_path):
     (["-o", "/tmp/x.png", "--bdepth", "-1", "x.rti"], "Error: Bounce depth must be non-negative."),
     (["-o", "/nonexistent_dir/x.png", "x.rti"], "Error: Output file is not writable."),
     (["-o", "/tmp/rtamd_cli_test.png", "/nonexistent.rti"], "Error: file not found: /nonexistent.rti"),
+    (["-o", "/tmp/x.png", "--gpus", "0", "x.rti"], "Error: GPU count is invalid."),
 ])
 def test_cli_option_errors_match_reference(args, msg):
     """options.cpp:18-86 / main.cpp:40-66 messages and exit status 1 (checked before any GPU use)."""
