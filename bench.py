@@ -4,7 +4,7 @@
 Workload (BASELINE.json configs[2], the metric's 1920x1080 single-GPU config):
 excess_inputs/bunny.rti (4,968-triangle bunny + reflective floor +
 mirror spheres), 1920x1080, --bdepth 4.  A step renders a fixed batch of frames
-(--frames-per-step, default 8) of that scene through the C-ABI (librtamd.so); rays =
+(--frames-per-step, default 32) of that scene through the C-ABI (librtamd.so); rays =
 traceRay calls (primary + reflection + refraction) + shadow rays, counted by the kernels
 and equal to the reference's counts.  Inputs (the scene) are resident in HBM before the
 timed region; every frame is written as the reference's f64 RasterImage and as RGB8.
@@ -387,16 +387,16 @@ def main():
     n_buf = max(rd.n_rows(H, k, ways, blk) for k in range(ways)) if partition else H
     outs = [torch.empty((n_buf, W, 3), dtype=torch.float64, device="cuda") for _ in range(B)]
     # RGB8 double-buffered: the gathers of step i (side stream) overlap the render of step i+1
-    out8s = [[torch.zeros((n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(B)] for _ in range(2)]
+    # (one tensor per buffer set: partition mode gathers all the step's frames in ONE collective)
+    out8s = [torch.zeros((B, n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
     gathered = [None, None]
     comm = torch.cuda.Stream() if world > 1 else torch.cuda.current_stream()
     prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rows[0], rows[1], rows[2], row_block=rows[3])
     stream = torch.cuda.current_stream().cuda_stream
-    gbufs = [torch.empty((n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
-        if rank == 0 and world > 1 else None
+    gbufs = [torch.empty((B, n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
+        if rank == 0 and world > 1 and partition else None
     n_frames_rank0 = B if partition else B * world
-    frames = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(n_frames_rank0)] \
-        if rank == 0 else None
+    frames = torch.empty((n_frames_rank0, H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
 
     totals = {"rays": 0, "trace_rays": 0, "zero": 0, "ms": [0.0] * 3, "launches": [0] * 3, "bytes": [0] * 3,
               "flops": [0] * 3}
@@ -408,22 +408,23 @@ def main():
         n_steps[0] += 1
         if gathered[k] is not None:  # the gathers that read these buffers two steps ago
             torch.cuda.current_stream().wait_event(gathered[k])
-        st = s.render_batch_device([prm] * B, [o.data_ptr() for o in outs], [o.data_ptr() for o in out8s[k]],
+        st = s.render_batch_device([prm] * B, [o.data_ptr() for o in outs], [out8s[k][f].data_ptr() for f in range(B)],
                                    stream)
         rendered = torch.cuda.Event()
         rendered.record()
         with torch.cuda.stream(comm):
             comm.wait_event(rendered)
-            for f in range(B):
-                if partition and ways != world:  # emulated share: no assembly
-                    pass
-                elif partition:  # frame f assembled on rank 0 from every rank's rows
-                    rd.gather_rows(out8s[k][f], H, dst=0, out=frames[f] if rank == 0 else None, bufs=gbufs,
-                                   block=blk)
-                elif world > 1:  # whole frames of every rank to rank 0
-                    rd.gather_frames(out8s[k][f], dst=0, out=frames[f * world:(f + 1) * world] if rank == 0 else None)
-                else:
-                    frames[f].copy_(out8s[k][f])
+            if partition and ways != world:  # emulated share: no assembly
+                pass
+            elif partition:  # every frame assembled on rank 0 from all ranks' rows: one gather per step
+                rd.gather_rows_batch(out8s[k], H, dst=0, out=frames, bufs=gbufs, block=blk)
+            else:
+                for f in range(B):
+                    if world > 1:  # whole frames of every rank to rank 0
+                        rd.gather_frames(out8s[k][f], dst=0,
+                                         out=[frames[f * world + r] for r in range(world)] if rank == 0 else None)
+                    else:
+                        frames[f].copy_(out8s[k][f])
             gathered[k] = torch.cuda.Event()
             gathered[k].record(comm)
         if record:
@@ -462,7 +463,7 @@ def main():
     for _ in range(max(0, a.latency_frames)):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        s.render_device(prm, outs[0].data_ptr(), out8s[0][0].data_ptr(), stream)
+        s.render_device(prm, outs[0].data_ptr(), out8s[0][0].data_ptr(), stream)  # (frame 0 of set 0)
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t1)
     lat = sorted(lat)[len(lat) // 2] if lat else float("nan")

@@ -92,6 +92,34 @@ def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
     return None
 
 
+def gather_rows_batch(local: torch.Tensor, height: int, dst: int = 0, out: Optional[torch.Tensor] = None,
+                      bufs: Optional[list] = None, block: int = 1) -> Optional[torch.Tensor]:
+    """A batch of frames in ONE collective: `local` (F, n_buf, W, C) holds this rank's rows
+    of F frames (n_buf >= its row count); on `dst`, out (F, H, W, C) receives every frame
+    assembled from all ranks' rows (row blocks of `block` rows, see rank_rows)."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rank = dist.get_rank() if dist.is_initialized() else 0
+    if world == 1:
+        if out is not None:
+            out.copy_(local[:, :height])
+        return out
+    staged = local.is_cuda and dist.get_backend() == "gloo"
+    src = local.cpu() if staged else local.contiguous()
+    if rank == dst:
+        if bufs is None or staged:
+            bufs = [torch.empty_like(src) for _ in range(world)]
+        dist.gather(src, bufs, dst=dst)
+        if out is None:
+            out = torch.empty((local.shape[0], height) + tuple(local.shape[2:]), dtype=local.dtype,
+                              device=local.device)
+        for r in range(world):
+            idx = _row_index(height, r, world, block, out.device)
+            out[:, idx] = bufs[r][:, : idx.numel()].to(out.device)
+        return out
+    dist.gather(src, None, dst=dst)
+    return None
+
+
 _ROW_INDEX = {}
 
 

@@ -102,3 +102,45 @@ def test_rotated_batch_assembles_every_frame(oracle, world):
     assert len(got) == world
     for fr in got:
         assert np.array_equal(fr, want)
+
+
+def _batch_rows_worker(rank, world, port, scene, w, h, bdepth, block, q):
+    import torch.distributed as dist
+    import pyoracle
+    from rtamd import dist as rd
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        full, _ = pyoracle.render(scene, w, h, bdepth=bdepth, threads=2)
+        rows = rd.rows_of(h, rank, world, block)
+        n_buf = max(rd.n_rows(h, k, world, block) for k in range(world))
+        local = torch.zeros((3, n_buf, w, 3), dtype=torch.float64)
+        for f in range(3):  # three frames: the image, scaled by 2 and by 3
+            local[f, : len(rows)] = torch.from_numpy(full[rows] * (f + 1))
+        out = rd.gather_rows_batch(local, h, block=block)
+        if rank == 0:
+            q.put(out.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,block", [(2, 8), (3, 4), (3, 1)])
+def test_batched_row_gather(oracle, world, block):
+    """bench.py's partition step: all frames of a step gathered in one collective and
+    de-interleaved on rank 0 (row blocks)."""
+    w, h, bdepth = 21, 29, 3
+    path = os.path.join(SCENES, "excess_inputs/bunny.rti")
+    want, _ = oracle.render(path, w, h, bdepth=bdepth)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_batch_rows_worker, args=(r, world, port, path, w, h, bdepth, block, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for f in range(3):
+        assert np.array_equal(got[f], want * (f + 1))
