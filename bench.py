@@ -335,7 +335,7 @@ def strong_scaling(a, world, rank, local, groups, dist, torch):
                         "partition": f"{blk}-row blocks interleaved (row r -> rank (r // {blk}) mod n), RGB8 rows "
                                      "gathered to rank 0 over "
                                      + ("RCCL" if dist.is_initialized() and dist.get_backend() == "nccl" else
-                                        "the process group" if world > 1 else "(no exchange at n = 1)"),
+                                        "the process group" if world > 1 else "nothing (one rank)"),
                         "curve": rows_curve}
         s.close()
     return out
@@ -483,9 +483,7 @@ def main():
     latency = max(v[3] for v in allv)
     zero_rays = sum(v[4] for v in allv)
     rank_ms = [v[5] / a.steps * 1e3 for v in allv]
-    conc_ms = [sum(v[6 + j] for v in allv) for j in range(3)]
     conc_launches = [sum(v[9 + j] for v in allv) for j in range(3)]
-    conc_bytes = [sum(v[12 + j] for v in allv) for j in range(3)]
 
     sweep = {}
     groups = []
@@ -500,10 +498,9 @@ def main():
     if rank == 0:
         fps = B if partition else B * world  # frames per step
         value = rays / elapsed / 1e6
-        concurrent = {"kernel_ms_per_frame": {STAGES[j]: round(conc_ms[j] / a.steps / fps, 4) for j in range(3)},
-                      "launches_per_frame": {STAGES[j]: conc_launches[j] / a.steps / fps for j in range(3)},
-                      "note": "HIP-event spans of the throughput schedule: launches of different levels and frames "
-                              "overlap, so these spans add up to more than the step; not a time base"}
+        # the throughput schedule replays launch plans without per-kernel events (api.cpp Plan):
+        # only the launch counts are known there; kernel times come from the solo pass
+        concurrent = {"launches_per_frame": {STAGES[j]: conc_launches[j] / a.steps / fps for j in range(3)}}
         res = {
             "metric": "Mrays/s (primary+secondary) and wall-clock at 1920x1080; HBM GB/s vs peak",
             "value": round(value, 3), "unit": "Mrays/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -540,9 +537,6 @@ def main():
             # the dominant kernel's solo time per step must fit in the step (a consistent time base)
             dom = res["roofline"]["kernel"]
             res["roofline"]["solo_ms_per_step"] = round(res["roofline"]["solo_ms_per_frame"][dom] * fps / world, 3)
-            res["roofline"]["concurrent"]["algorithmic_GBps_event_spans"] = round(
-                conc_bytes[STAGES.index(dom)] / (conc_ms[STAGES.index(dom)] * 1e-3) / 1e9, 1) \
-                if conc_ms[STAGES.index(dom)] else None
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(s, scene, W, H, kw["bdepth"], a.cpu_seconds)
             same = same_algorithm_baseline(scene, W, H, kw["bdepth"], a.cpu_seconds / 3)

@@ -18,6 +18,19 @@
 #ifndef RT_PHASE_PROF
 #define RT_PHASE_PROF 0
 #endif
+// Diagnostic builds only (tools/valu_breakdown.sh; the images are WRONG): skip a part of the
+// packet kernels to measure its share of the vector instructions.  bit 0: the packet LBVH
+// searches find nothing; bit 1: packet face tests skipped (node walk only); bit 2:
+// occluded_packet decides nothing (returns false after the may-raise check).
+#ifndef RT_DIAG_SKIP
+#define RT_DIAG_SKIP 0
+#endif
+// Facing pre-test (face_facing_rejects): exact skip of a face whose facing test certainly
+// fails, before its fp64 Cramer test.  0: off (A/B builds).  (A planar-geometry form, one
+// world-space dot product per geometry before its transform, measured -1.4 %: DESIGN.md.)
+#ifndef RT_FACING
+#define RT_FACING 1
+#endif
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include "device_types.h"
@@ -207,6 +220,30 @@ __device__ __forceinline__ bool quotient_surely_above(double num, double den, do
 	return ((num < 0) == (den < 0)) && thr >= 0x1p-1000 && fabs(num) > thr;
 }
 
+// ------------------------------------------------------------- facing pre-tests (exact)
+// The reference accepts a face only if its interpolated normal tn = (w0 n0 + a n1) + b n2
+// (w0 = (1 - a) - b, a, b in [0, 1]) passes the facing test `!front ^ reverse` with
+// front = dot(tn, d) < 0 (geometry.cpp:117-122), after the whole Cramer test.  When
+// dot(n_i, d) has one sign, with a margin, for all three vertex normals, so has dot(tn, d)
+// (a convex combination; its rounding errs by ~10 ulp of sum w_i |n_i| |d|, far below the
+// margins), and the facing test's outcome is known before any of the face's fp64 work.
+// NaN or infinite barycentrics never reach acceptance (t and the distance are then NaN or
+// infinite and fail the distance test), so only finite a, b matter.
+
+// True when the facing test certainly rejects face F for the object-space unit direction d
+// (|d| within 1e-15 of 1): every vertex normal lies within r of the fp32 vector c, so
+// dot(n_i, d) lies within r of dot(c, d); the fp32 dot product of c with d rounded to fp32
+// errs by < 5e-7 |c|_1, and tau = r + 2 (1e-5 max |n_i|_1 + 1e-6 |c|_1) (bvh.cpp
+// facing_data) leaves every dot(n_i, d) beyond 1e-5 |n_i|_1 with the sign of dot(c, d).
+// tau = +inf disables the face's test, a NaN compares false: never a rejection.
+template <typename FP>
+__device__ __forceinline__ bool face_facing_rejects(FP F, V3 d, bool reverse) {
+	const float s = fmaf(F->cone_c[2], static_cast<float>(d.z),
+	                     fmaf(F->cone_c[1], static_cast<float>(d.y), F->cone_c[0] * static_cast<float>(d.x)));
+	const float tau = F->cone_tau;
+	// s > tau: front false, rejected unless reverse; s < -tau: front true, rejected if reverse
+	return reverse ? s < -tau : s > tau;
+}
 // One iteration of the face loop of geometry.cpp:78-124.  Accepts the face when it is
 // strictly closer, or equally close with a smaller reference index: over any visiting
 // order this selects the same face as the reference's in-order scan.
@@ -216,6 +253,7 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
                                           double any_limit, MeshBest& best, WorkStats& ws) {
 	ws.inc<W_TRIS>();
 	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
+	if (RT_FACING && face_facing_rejects(F, d, reverse)) return false;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	// id is fetched with the vertices: the compiler would otherwise issue its load where
 	// it is first used (one more memory round trip per candidate face)
@@ -667,7 +705,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					live = false;
 				}
 				PROF_END(ws, PH_FACES, tf);
-		} else {
+		} else if (!(RT_DIAG_SKIP & 1)) {
 			if (live) ws.inc<W_ENTRIES>();
 			const V3 inv = safe_inv(d);
 			const Ray32 r32 = ray32(G, o, d, inv);
@@ -705,7 +743,8 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					if (k == 1) want = want && live && (c ? tn1 : tn0) <= lim;
 					if (!wave_any(want)) continue;
 					const int32_t cf = uniform_i32(c ? rf1 : rf0), cc = uniform_i32(c ? rc1 : rc0);
-					if (cc > 0) {
+					if (cc > 0 && (RT_DIAG_SKIP & 2)) {
+					} else if (cc > 0) {
 						PROF_BEGIN(tf);
 						const int32_t f0 = G->face_begin + cf;
 						for (int32_t f = f0; f < f0 + cc; f++)
@@ -797,6 +836,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 	const bool inf_light = dist_light == INFINITY;
 	bool occ = false;
 	check_may_raise(S, d, on, ctr);
+	if (RT_DIAG_SKIP & 4) return false;
 	for (int k = 0; k < S.n_geoms; k++) {
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;

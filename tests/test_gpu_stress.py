@@ -138,3 +138,47 @@ def test_zero_phong_terms_lights_behind(gpu, oracle, tmp_path, kd, ks, ns):
             "sph   1.6 0.2 -1.0 0.6\n" + "tri   -4 -1.2 4   4 -1.2 4   4 -1.2 -4\n")
     st = check(gpu, oracle, scene(tmp_path, "behind", body), w=48, h=36, bdepth=3, bits=True)
     assert (st.shadow_rays_zero_terms > 0) == (ns > 0)
+
+
+def write_normal_soup(path, n, seed, mode):
+    """Triangle soup with per-vertex normals for the facing pre-test (intersect.h
+    face_facing_rejects): 'spread' three unrelated normals per face (wide cones), 'grazing'
+    one normal nearly perpendicular to the view axis with 1e-7 per-vertex jitter (narrow
+    cones whose facing sign flips across the image), 'scaled' normals of magnitudes 1e-9 to
+    1e3 (faces whose pre-test is disabled) and 'flipped' vertex normals opposite to each
+    other (interpolated normal through zero)."""
+    rng = np.random.default_rng(seed)
+    v, vn, f = [], [], []
+    for i in range(n):
+        c = rng.uniform(-1.2, 1.2, 3) * np.array([1.0, 0.8, 0.5])
+        pts = [c + rng.uniform(-0.25, 0.25, 3) for _ in range(3)]
+        if mode == "spread":
+            ns = [rng.normal(size=3) for _ in range(3)]
+        elif mode == "grazing":
+            base = np.array([rng.normal(), rng.normal(), rng.uniform(-1e-3, 1e-3)])
+            ns = [base + rng.normal(size=3) * 1e-7 for _ in range(3)]
+        elif mode == "scaled":
+            base = rng.normal(size=3)
+            ns = [base * s for s in rng.choice([1e-9, 1e-3, 1.0, 1e3], 3)]
+        else:  # flipped
+            base = rng.normal(size=3)
+            ns = [base, -base, base * rng.uniform(0.5, 2.0)]
+        for p, q in zip(pts, ns):
+            v.append("v %.17g %.17g %.17g" % tuple(p))
+            vn.append("vn %.17g %.17g %.17g" % tuple(q))
+        k = 3 * i
+        f.append("f %d//%d %d//%d %d//%d" % (k + 1, k + 1, k + 2, k + 2, k + 3, k + 3))
+    path.write_text("\n".join(v + vn + f) + "\n")
+
+
+@pytest.mark.parametrize("mode", ["spread", "grazing", "scaled", "flipped"])
+def test_facing_pretest_vertex_normals(gpu, oracle, tmp_path, mode):
+    """Faces are skipped before their fp64 Cramer test when the facing test certainly fails
+    (normal cones): bit-exact on meshes whose vertex normals differ, sit near
+    the facing boundary, have wildly different magnitudes or cancel -- camera rays, shadow
+    rays from both sides, mirror and glass secondary rays."""
+    write_normal_soup(tmp_path / "nsoup.obj", 400, seed=7, mode=mode)
+    body = ("cam   0 0 6   -1.5 -1.1 2    1.5 -1.1 2   -1.5 1.1 2   1.5 1.1 2\n" + LIGHTS +
+            "ltp   0 0 -5 0.3 0.3 0.3\n" + MAT_SHINY + 'obj   "nsoup.obj"\n' + MAT_GLASS +
+            "sph   0.3 -0.2 1.5 0.5\n" + MAT_MIRROR + "sph   -1.6 0.9 -1.5 0.7\n")
+    check(gpu, oracle, scene(tmp_path, "nsoup_" + mode, body), w=64, h=48, bdepth=4, bits=True)

@@ -8,7 +8,7 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp
 cd /tmp
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $O/p1 -o pmc --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/p1.log 2>&1 || exit 1
-timeout -k 10 240 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_BUSY_CYCLES SQ_INSTS_SMEM -d $O/p2 -o pmc --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/p2.log 2>&1 || exit 2
-timeout -k 10 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_FMA_F64 -d $O/p3 -o pmc --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/p3.log 2>&1 || exit 3
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --pmc SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $O/p1 -o pmc --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --sweep "" --solo-frames 0 --latency-frames 0 > $O/p1.log 2>&1 || exit 1
+timeout -k 10 240 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_BUSY_CYCLES SQ_INSTS_SMEM -d $O/p2 -o pmc --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --sweep "" --solo-frames 0 --latency-frames 0 > $O/p2.log 2>&1 || exit 2
+timeout -k 10 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TCC_READ_REQ_sum SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_FMA_F64 -d $O/p3 -o pmc --output-format csv -- python $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --sweep "" --solo-frames 0 --latency-frames 0 > $O/p3.log 2>&1 || exit 3
 echo done

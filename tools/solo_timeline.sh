@@ -9,5 +9,5 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 export TMPDIR=/tmp RTAMD_SERIAL=1
 cd /tmp
-timeout -k 10 200 rocprofv3 --kernel-trace -d $O/kt -o kt --output-format csv -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-frames 0 --frames-per-gpu 1 > $O/kt.log 2>&1 || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace -d $O/kt -o kt --output-format csv -- python $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-frames 0 --frames-per-step 1 --sweep "" --solo-frames 0 > $O/kt.log 2>&1 || exit 1
 python $R/tools/frame_timeline.py $O/kt/kt_kernel_trace.csv > $O/timeline.txt
