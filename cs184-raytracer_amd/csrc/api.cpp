@@ -102,11 +102,12 @@ struct LevelBuffers {
 // render is redone host-driven.
 struct PlanKey {
 	int32_t width, height, depth, io;
+	int32_t direct_levels;  // the schedule's split of direct and batched shading (a graph bakes it in)
 	int64_t n0;
 	uint64_t rows_hash;  // the chunk's image rows (they decide the level counts)
 	bool operator==(const PlanKey& o) const {
-		return width == o.width && height == o.height && depth == o.depth && io == o.io && n0 == o.n0 &&
-		       rows_hash == o.rows_hash;
+		return width == o.width && height == o.height && depth == o.depth && io == o.io &&
+		       direct_levels == o.direct_levels && n0 == o.n0 && rows_hash == o.rows_hash;
 	}
 };
 
@@ -187,7 +188,12 @@ struct rt_scene {
 	int64_t out8_capacity = 0;
 	int fail_after = -1;                         // fault injection (rt_debug_fail_after): launches left
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
-	int direct_levels = 2;                       // RTAMD_DIRECT_LEVELS (measured best on C3)
+	// RTAMD_DIRECT_LEVELS: levels shaded beside the closest-hit chain; the rest are shaded in
+	// batches after it.  Measured best on C3: 2 for one frame per call
+	// (latency: level 1's shading overlaps levels 2+), 1 for batches (throughput: fewer,
+	// larger shading launches while other frames fill the GPU).  The variable sets both.
+	int direct_levels_single = 2;
+	int direct_levels_batch = 1;
 	int single_lanes = 1;                        // lanes one frame is split over (RTAMD_LANES)
 	int batch_lanes = 3;                         // frames of a batch in flight (RTAMD_BATCH_LANES)
 	int prio_low = 0, prio_high = 0;
@@ -200,7 +206,7 @@ struct rt_scene {
 	int graphs = 2;
 	int64_t batch_chunk_pixels = (int64_t)1 << 22;  // RTAMD_BATCH_CHUNK: most pixels of a chunk packed from several jobs
 	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
-	int shadow_all_lights = 1;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
+	int shadow_all_lights = 3;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// measured best on C3: packets for the camera rays and their first bounce, and
 	// for the shadow rays of both (once the zero-term decision thinned the per-lane waves)
 	int packet_mask =
@@ -349,6 +355,7 @@ int32_t selected_row(const rt_render_params* p, int64_t q) {
 // events complete.
 struct Render {
 	rt_scene* s;
+	int direct_levels = 2;  // rt_scene::direct_levels_single or _batch, for this call
 	rt_counters cnt{};
 	float kernel_ms = 0.f;
 	Progress* progress = nullptr;
@@ -422,6 +429,7 @@ struct Render {
 		k.height = ln.fg.height;
 		k.depth = ln.depth;
 		k.io = ln.io;
+		k.direct_levels = direct_levels;
 		k.n0 = ln.n0;
 		k.rows_hash = ln.rows_hash;
 		return k;
@@ -503,7 +511,7 @@ struct Render {
 			step(done ? hipEventRecord(done, st) : hipErrorOutOfMemory);
 			// shading beside the chain only where a later level's tracing can overlap it: a
 			// wait on a not yet signalled event of another queue costs tens of microseconds
-			if (L < s->direct_levels && rc == RT_OK) {
+			if (L < direct_levels && rc == RT_OK) {
 				const bool side = L < nlev - 1;
 				hipStream_t q = side ? ln.shade[L % 3] : st;
 				if (side) step(hipStreamWaitEvent(q, done, 0));
@@ -519,10 +527,10 @@ struct Render {
 			}
 		}
 		// the deep levels after the chain, on its own stream (the reductions wait for them)
-		if (rc == RT_OK && nlev > s->direct_levels) {
+		if (rc == RT_OK && nlev > direct_levels) {
 			hipStream_t q = st;
 			std::vector<int> deep;
-			for (int L = s->direct_levels; L < nlev; L++) deep.push_back(L);
+			for (int L = direct_levels; L < nlev; L++) deep.push_back(L);
 			for (size_t k = 0; k < deep.size() && rc == RT_OK; k += rtamd::kMaxBatch) {
 				const size_t e = std::min(deep.size(), k + rtamd::kMaxBatch);
 				scratch.launches[1] = scratch.launches[2] = 0;
@@ -664,7 +672,7 @@ struct Render {
 				return rc;
 		}
 		if (nh > 0) {
-			if (L < s->direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
+			if (L < direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
 				if ((rc = launch_shading(ln, {{L, nh}}, ln.shade[L % 3]))) return rc;
 			} else {
 				ln.deferred.push_back({L, nh});
@@ -982,7 +990,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	s->device = device;
 	// tuning knobs; lanes are created on first use
 	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);
-	if (const char* dl = std::getenv("RTAMD_DIRECT_LEVELS")) s->direct_levels = std::max(1, std::atoi(dl));
+	if (const char* dl = std::getenv("RTAMD_DIRECT_LEVELS"))
+		s->direct_levels_single = s->direct_levels_batch = std::max(1, std::atoi(dl));
 	if (const char* nl = std::getenv("RTAMD_LANES")) s->single_lanes = std::min(kMaxLanes, std::max(1, std::atoi(nl)));
 	if (const char* bl = std::getenv("RTAMD_BATCH_LANES"))
 		s->batch_lanes = std::min(kMaxLanes, std::max(1, std::atoi(bl)));
@@ -1137,6 +1146,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	int rc = ensure_lanes(s, n_lanes);
 	if (rc) return rc;
 	Render R{s};
+	R.direct_levels = batch ? s->direct_levels_batch : s->direct_levels_single;
 	R.progress = progress;
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
 	// the caller's stream is joined first (its prior work, e.g. the allocation of the

@@ -185,6 +185,27 @@ __device__ __forceinline__ uint32_t prof_t() {
 #define PROF_END(ws, k, v) ((void)0)
 #endif
 
+#ifndef RT_DIAG_LANES
+#define RT_DIAG_LANES 0
+#endif
+// RT_DIAG_GEOMS (diagnostic build): per shadow-order position k, [2k] 64 x the packet
+// shadow waves with a candidate lane there, [2k + 1] the candidate lanes
+#ifndef RT_DIAG_GEOMS
+#define RT_DIAG_GEOMS 0
+#endif
+#if RT_PHASE_PROF || RT_DIAG_LANES || RT_DIAG_GEOMS
+// RT_PHASE_PROF: [stage * 2 + packet][slot] shader cycles; RT_DIAG_LANES (diagnostic build):
+// lane occupancy of the per-lane kernels, read by tools/lane_census.py
+__device__ unsigned long long g_phase[4 * kPhaseSlots];
+__device__ __forceinline__ void diag_lanes(int slot, bool p) {
+	const unsigned long long m = __ballot(p);
+	if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) {
+		atomicAdd(&g_phase[slot], 64ull);
+		atomicAdd(&g_phase[slot + 1], (unsigned long long)__popcll(m));
+	}
+}
+#endif
+
 // A mesh hit (face, barycentric a, b), or a sphere hit (face -1, ray parameter t in a)
 struct FaceHit {
 	int32_t face;
@@ -405,6 +426,9 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		// <= -2 a leaf (face offset << 3 | count), -1 done.  The far child of a node whose
 		// two children are hit is pushed (LDS stack, kStackDepth entries per lane).
 		ws.inc<W_ENTRIES>();
+#if RT_DIAG_LANES
+		diag_lanes(kAnyHit ? 24 : 8, true);  // wave slots and lanes entering a per-lane LBVH search
+#endif
 		const V3 inv = safe_inv(d);
 		const Ray32 r32 = ray32(G, o, d, inv);
 		// the node-pruning limit in the shifted fp32 frame; it changes only with best.dist
@@ -449,6 +473,9 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 				}
 				if (RT_SPECULATIVE && __ballot(leaf == -1) == 0) break;  // every walking lane holds a leaf
 			}
+#if RT_DIAG_LANES
+			diag_lanes(kAnyHit ? 26 : 10, leaf != -1);  // lanes holding a leaf when the face phase starts
+#endif
 			PROF_END(ws, PH_NODES, tn);
 			if (!RT_SPECULATIVE && ref <= -2) {
 				leaf = ref;
@@ -845,6 +872,9 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		const bool cand = on && !occ && slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
+#if RT_DIAG_GEOMS
+		if (k < 16) diag_lanes(2 * k, cand);
+#endif
 		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);

@@ -125,9 +125,7 @@ __device__ __forceinline__ unsigned long long* shard(unsigned long long* stats) 
 	return stats + (blockIdx.x % kStatShards) * kStatStride;
 }
 
-#if RT_PHASE_PROF
-__device__ unsigned long long g_phase[4 * kPhaseSlots];  // [stage * 2 + packet][slot]
-#endif
+
 
 __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long long* stats, int stage, int packet = 0) {
 #if RT_PHASE_PROF
@@ -217,6 +215,9 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	PROF_BEGIN(t_setup);
 	if (active) level_ray(S, fg, level, i, cur, o, d, inside, ctr);
 	PROF_END(ws, PH_SETUP, t_setup);
+#if RT_DIAG_LANES
+	if (!kPacket) diag_lanes(0, active);  // [0] wave slots, [1] active lanes of k_closest<false>
+#endif
 	if (kPacket)
 		hit = closest_hit_packet(S, o, d, inside, active, dist, gi, P, Nobj, stack, ctr, ws);
 	else if (active)
@@ -523,6 +524,12 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 			PROF_END(ws, PH_SETUP, t_total);
 		}
 		const bool trace = on && !zero;
+#if RT_DIAG_LANES
+		if (!kPacket) {
+			diag_lanes(16, on);     // [16] wave slots, [17] lanes with a hit of this level
+			diag_lanes(18, trace);  // [18] wave slots, [19] lanes tracing (zero-term decided excluded)
+		}
+#endif
 		bool occ = false;
 		if (kPacket)
 			occ = occluded_packet(S, P, Ld, rev, dL, trace, stack, ctr, ws);
@@ -840,11 +847,11 @@ hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uin
 }
 
 hipError_t read_phase_profile(unsigned long long* out) {
-#if RT_PHASE_PROF
-	hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase));
+#if RT_PHASE_PROF || RT_DIAG_LANES || RT_DIAG_GEOMS
+	hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dev::g_phase), sizeof(dev::g_phase));
 	if (e != hipSuccess) return e;
 	static const unsigned long long zero[4 * kPhaseSlots] = {};
-	return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), zero, sizeof(zero));
+	return hipMemcpyToSymbol(HIP_SYMBOL(dev::g_phase), zero, sizeof(zero));
 #else
 	for (int k = 0; k < 4 * kPhaseSlots; k++) out[k] = 0;
 	return hipSuccess;
