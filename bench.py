@@ -74,8 +74,9 @@ def parse():
     ap.add_argument("--sweep", default="C5_refraction3_4096_bd8,C4_airboat_sub_1920x1080",
                     help="configs whose single frame is row-partitioned over 1, 2, 4, 8 ranks ('' = none)")
     ap.add_argument("--sweep-reps", type=int, default=3)
-    ap.add_argument("--solo-frames", type=int, default=3,
-                    help="frames rendered with every kernel alone (RTAMD_SERIAL=1) for the roofline time base")
+    ap.add_argument("--solo-frames", type=int, default=4,
+                    help="frames rendered (one batch call) with every kernel alone (RTAMD_SERIAL=1) for the roofline "
+                         "time base")
     ap.add_argument("--solo-only", action="store_true",
                     help="run only the solo pass (the command rocprofv3 profiles for the roofline)")
     ap.add_argument("--latency-frames", type=int, default=5,
@@ -86,6 +87,11 @@ def parse():
                     help="PMC-measured HBM bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE); default: the "
                          "latest profiles/round*/traffic.json")
     return ap.parse_args()
+
+
+def latest_valu():
+    cands = sorted(glob.glob(os.path.join(REPO, "profiles", "round*", "valu.json")))
+    return cands[-1] if cands else None
 
 
 def latest_traffic():
@@ -178,43 +184,47 @@ def stage_work(st):
 
 
 def solo_pass(scene_path, W, H, kw, frames, device):
-    """Every kernel alone: a scene created with RTAMD_SERIAL=1 runs the shading kernels on the
-    closest-hit chain's stream, so the HIP events around each launch bracket that kernel and
-    nothing else (the throughput schedule overlaps levels and frames)."""
+    """Every kernel alone, in the bench's own (batch) schedule: `frames` frames in ONE
+    rt_render_batch_device call on a scene created with RTAMD_SERIAL=1 (the shading kernels
+    on the closest-hit chain's stream) and RTAMD_BATCH_LANES=1 (one pipeline), so the HIP
+    events around each launch bracket that kernel and nothing else, while the batch-mode
+    schedule (frames packed into shared chunks, direct/deferred shading split) is the one the
+    timed steps run concurrently."""
     import rtamd
     import torch
-    old = os.environ.get("RTAMD_SERIAL")
-    os.environ["RTAMD_SERIAL"] = "1"
+    keep = {k: os.environ.get(k) for k in ("RTAMD_SERIAL", "RTAMD_BATCH_LANES")}
+    os.environ.update({"RTAMD_SERIAL": "1", "RTAMD_BATCH_LANES": "1"})
     try:
         s = rtamd.load_scene(scene_path, device=device)
         s.upload()
     finally:
-        if old is None:
-            del os.environ["RTAMD_SERIAL"]
-        else:
-            os.environ["RTAMD_SERIAL"] = old
-    out = torch.empty((H, W, 3), dtype=torch.float64, device="cuda")
-    out8 = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
-    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)
+        for k, v in keep.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    outs = [torch.empty((H, W, 3), dtype=torch.float64, device="cuda") for _ in range(frames)]
+    out8s = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(frames)]
+    prm = [s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)] * frames
     stream = torch.cuda.current_stream().cuda_stream
-    s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)  # allocations
+    ptrs = ([o.data_ptr() for o in outs], [o.data_ptr() for o in out8s])
+    s.render_batch_device(prm, *ptrs, stream)  # allocations
     acc = {"ms": [0.0] * 3, "launches": [0] * 3, "bytes": [0] * 3, "flops": [0] * 3, "wall": 0.0}
-    for _ in range(frames):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        st = s.render_device(prm, out.data_ptr(), out8.data_ptr(), stream)
-        acc["wall"] += time.perf_counter() - t0
-        nb, fl = stage_work(st)
-        for k in range(3):
-            acc["ms"][k] += st.stage_ms[k]
-            acc["launches"][k] += st.stage_launches[k]
-            acc["bytes"][k] += nb[k]
-            acc["flops"][k] += fl[k]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = s.render_batch_device(prm, *ptrs, stream)
+    acc["wall"] += time.perf_counter() - t0
+    nb, fl = stage_work(st)
+    for k in range(3):
+        acc["ms"][k] += st.stage_ms[k]
+        acc["launches"][k] += st.stage_launches[k]
+        acc["bytes"][k] += nb[k]
+        acc["flops"][k] += fl[k]
     s.close()
     return acc
 
 
-def roofline(solo, frames, traffic_path, concurrent):
+def roofline(solo, frames, traffic_path, concurrent, valu_path=None):
     """Dominant kernel (largest solo time per frame) against three roofs; `bound` = the roof
     it is closest to.  achieved / peak / frac are that roof's; every fraction is listed."""
     dom = max(range(3), key=lambda k: solo["ms"][k])
@@ -238,6 +248,18 @@ def roofline(solo, frames, traffic_path, concurrent):
         "fp64": {"achieved": flops / t_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                  "what": "SURVEY.md §8d algorithmic FP64 flops / solo launch time vs vector FP64 peak"},
     }
+    if valu_path and os.path.exists(valu_path):
+        try:
+            vj = json.load(open(valu_path))
+            vpl = vj.get("valu_per_launch", {}).get(name)
+            if vpl and vj.get("peak_wave_instr_per_s"):
+                roofs["valu"] = {"achieved": vpl / t_launch_s / 1e9, "peak": vj["peak_wave_instr_per_s"] / 1e9,
+                                 "unit": "G wave-instr/s",
+                                 "what": "PMC SQ_INSTS_VALU per launch (wave64 vector instructions, " +
+                                         os.path.relpath(valu_path, REPO) + ") / solo launch time vs the sustained "
+                                         "v_fma_f32 issue rate of the whole chip (tools/valu_calibration.py)"}
+        except (OSError, ValueError):
+            pass
     if traffic:
         roofs["hbm"] = {"achieved": traffic / t_launch_s / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "what": "PMC HBM bytes per launch (FETCH_SIZE, WRITE_SIZE; profiles/) / solo launch time"}
@@ -250,9 +272,9 @@ def roofline(solo, frames, traffic_path, concurrent):
     return {
         "bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"], "frac": b["frac"],
         "traffic": traffic, "kernel": name,
-        "time_base": f"solo: {frames} frames with RTAMD_SERIAL=1 (every kernel alone on one stream), HIP events "
-                     "around each launch on that stream; rocprofv3 of `bench.py --solo-only` gives the same "
-                     "durations (profiles/)",
+        "time_base": f"solo: {frames} frames in one batch call (the bench's schedule) with RTAMD_SERIAL=1 and "
+                     "RTAMD_BATCH_LANES=1 (every kernel alone on one stream), HIP events around each launch on that "
+                     "stream; rocprofv3 of `bench.py --solo-only` gives the same durations (profiles/)",
         "avg_launch_ms": round(t_launch_s * 1e3, 4), "launches_per_frame": launches / frames,
         "algorithmic_bytes_per_launch": round(alg_bytes), "fp64_flops_per_launch": round(flops),
         "hbm_algorithmic": {"achieved": round(alg_bytes / t_launch_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -369,7 +391,8 @@ def main():
         solo = solo_pass(scene, W, H, kw, a.solo_frames, local)
         if rank == 0:
             print(json.dumps({"solo_only": True, "config": a.config,
-                              "roofline": roofline(solo, a.solo_frames, traffic_path, None)}), flush=True)
+                              "roofline": roofline(solo, a.solo_frames, traffic_path, None, latest_valu())}),
+                  flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -529,7 +552,7 @@ def main():
                                        else f"frame-parallel: {B} whole frames per GPU per step, gathered to rank 0")},
             "per_rank": {"ms_per_step": [round(x, 3) for x in rank_ms],
                          "imbalance": round(max(rank_ms) / (sum(rank_ms) / len(rank_ms)), 3)},
-            "roofline": roofline(solo, a.solo_frames, traffic_path, concurrent) if solo else None,
+            "roofline": roofline(solo, a.solo_frames, traffic_path, concurrent, latest_valu()) if solo else None,
             "work_per_frame_rank0": work,
             "strong_scaling": sweep,
         }

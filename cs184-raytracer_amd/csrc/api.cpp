@@ -1553,6 +1553,29 @@ int rt_debug_fetch_calibration(int device, int64_t bytes) {
 	return RT_OK;
 }
 
+// Diagnostic (not in rtamd.h): VALU issue calibration.  k_valu_peak<float> and <double>
+// dispatches of `iters` rounds at 16 and 32 waves per CU (each after a warm-up); profiled with
+// rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace, instructions / duration is the sustained
+// wave64 VALU issue rate of fma chains (tools/valu_calibration.py).
+int rt_debug_valu_calibration(int device, int iters) {
+	HIP_TRY(hipSetDevice(device));
+	struct Sink {
+		void* p = nullptr;
+		~Sink() {
+			if (p) (void)hipFree(p);
+		}
+	} sink;
+	HIP_TRY(hipMalloc(&sink.p, 64));
+	// fp32 and fp64 chains at 16 and 32 waves per CU (4 and 8 per SIMD)
+	for (int f64 = 0; f64 < 2; f64++)
+		for (int waves = 16; waves <= 32; waves *= 2) {
+			HIP_TRY(rtamd::launch_valu_peak(iters / 8 + 1, f64, waves, sink.p, nullptr));  // warm-up (clocks)
+			HIP_TRY(rtamd::launch_valu_peak(iters, f64, waves, sink.p, nullptr));
+		}
+	HIP_TRY(hipDeviceSynchronize());
+	return RT_OK;
+}
+
 // Diagnostic (not in rtamd.h): the scene's next render fails after `launches` more
 // closest-hit launches, as a device failure in the middle of a render would (tests of the
 // error path: the render after it must be complete and exact).  -1 disables.

@@ -742,6 +742,31 @@ __global__ void k_stream_read(const T* __restrict__ p, int64_t n, unsigned long 
 	if (acc == 0x7fffffffffffffffull) sink[0] = acc;  // keeps the loads; never true for the zeroed buffer
 }
 
+// VALU issue calibration (tools/valu_calibration.py, profiles/): every wave runs `iters`
+// rounds of 8 independent fma chains in T, 16 waves per CU on every CU, nothing else: the
+// chip's sustained rate of wave64 vector instructions of that kind (SQ_INSTS_VALU per
+// second), the peak of the roofline's VALU roof.
+template <typename T>
+__global__ void __launch_bounds__(256) k_valu_peak(int iters, T seed, T* sink) {
+	T a[8];
+#pragma unroll
+	for (int k = 0; k < 8; k++) a[k] = seed + static_cast<T>(threadIdx.x + k);
+	const T m = static_cast<T>(0.999), c = static_cast<T>(1e-3);
+	for (int i = 0; i < iters; i++) {
+#pragma unroll
+		for (int k = 0; k < 8; k++) {
+			if constexpr (sizeof(T) == 4)  // one v_fma_f32 each (no v_pk_fma_f32 pairing)
+				asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(m), "v"(c));
+			else
+				a[k] = fma(a[k], m, c);
+		}
+	}
+	T acc = 0;
+#pragma unroll
+	for (int k = 0; k < 8; k++) acc += a[k];
+	if (acc == static_cast<T>(-1)) sink[0] = acc;  // keeps the chains; never true
+}
+
 // multi-GPU image assembly on the first device: one thread per byte of the image, each
 // row copied from its owner's buffer (partition_row)
 __global__ void k_deinterleave(uint8_t* dst, RowSources s, int n, int block, int64_t height, int64_t row_bytes) {
@@ -866,6 +891,15 @@ hipError_t launch_stream_read(const void* buf, int64_t bytes, int width, unsigne
 		case 8: hipLaunchKernelGGL(k_stream_read<uint64_t>, dim3(grid), dim3(256), 0, stream, (const uint64_t*)buf, bytes / 8, sink); break;
 		default: hipLaunchKernelGGL(k_stream_read<uint4>, dim3(grid), dim3(256), 0, stream, (const uint4*)buf, bytes / 16, sink); break;
 	}
+	return hipGetLastError();
+}
+
+hipError_t launch_valu_peak(int iters, bool f64, int waves_per_cu, void* sink, hipStream_t stream) {
+	const unsigned grid = 256 * std::max(1, waves_per_cu / 4);  // blocks of 4 waves on every CU
+	if (f64)
+		hipLaunchKernelGGL(k_valu_peak<double>, dim3(grid), dim3(256), 0, stream, iters, 1.0, static_cast<double*>(sink));
+	else
+		hipLaunchKernelGGL(k_valu_peak<float>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, static_cast<float*>(sink));
 	return hipGetLastError();
 }
 
