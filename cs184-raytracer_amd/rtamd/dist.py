@@ -1,8 +1,9 @@
 """Multi-GPU frame partition for the render path: one process per GPU, RCCL over xGMI.
 
 The reference renders one image with a thread pool over 2000-pixel blocks
-(scene.cpp:13-48).  Here a frame is split row-interleaved over the ranks (row r is
-rendered by rank r mod N: the costly glass/mirror regions of a frame are spread evenly),
+(scene.cpp:13-48).  Here a frame is split into blocks of B rows (bench.py: B = 8, so the
+8x8 ray tiles stay whole) interleaved over the ranks (row r is rendered by rank
+(r // B) mod N: the costly glass/mirror regions of a frame are spread evenly),
 each rank renders its rows on its own GPU (scene replicated in every GPU's HBM), and the
 RGB8 rows are gathered to rank 0 — the only data-path exchange.  --intersection-only
 needs one more collective: the reference normalises by the maximum over the whole image
