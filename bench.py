@@ -89,6 +89,22 @@ def parse():
     return ap.parse_args()
 
 
+class stdout_to_stderr:
+    """fd 1 -> fd 2 for the block: communication libraries print connection notices on
+    stdout (gloo: "[Gloo] Rank 0 is connected to ..."), and rank 0's stdout must hold only
+    the one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def latest_valu():
     cands = sorted(glob.glob(os.path.join(REPO, "profiles", "round*", "valu.json")))
     return cands[-1] if cands else None
@@ -378,10 +394,12 @@ def main():
         local = local % torch.cuda.device_count()  # rehearsal: several ranks may share a GPU
     torch.cuda.set_device(local)
     if world > 1:
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        with stdout_to_stderr():
+            if a.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
+            dist.barrier()  # the connections are made (and reported) here
     scene_rel, W, H, flags = CONFIGS[a.config]
     kw = option_kwargs(flags)
     scene = os.path.join(SCENES, scene_rel)
@@ -512,7 +530,8 @@ def main():
     groups = []
     n = 1
     while n <= world:
-        groups.append((n, dist.new_group(list(range(n))) if world > 1 and n > 1 else None))
+        with stdout_to_stderr():
+            groups.append((n, dist.new_group(list(range(n))) if world > 1 and n > 1 else None))
         n *= 2
     if a.sweep:
         sweep = strong_scaling(a, world, rank, local, groups, dist, torch)
