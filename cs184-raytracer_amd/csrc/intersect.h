@@ -341,11 +341,20 @@ __device__ __forceinline__ V3 safe_inv(V3 d) { return mk(slab_rcp(d.x), slab_rcp
 
 __device__ __forceinline__ double prune_limit(double best_dist) { return best_dist * (1.0 + 4e-9); }
 
+// Relative widening of the fp32 slab interval (round 1).  Not needed, per axis a (below):
+// the computed plane parameter fma(lo, I, -fl(o' I)) errs from (lo - o') / d_a by at most
+// 2^-23 |I| |o'_a| + 2^-23 |t| <= 1.5 * 2^-22 amax |I| (|o'_a|, |lo| <= amax, so |t| <= 2
+// amax |I|), while a face point inside the unpadded child box lies >= 2^-18 amax |I| in t
+// from each padded plane: the test keeps every box such a point is in, with a margin of
+// ten, without it.  1 restores the widening (A/B builds).
+#ifndef RT_SLAB32_WIDEN
+#define RT_SLAB32_WIDEN 0
+#endif
 // fp32 node test.  The ray origin is first moved along the ray to where it enters the
 // mesh's box (o' = o + s d, s >= 0; no face lies before it), so |o'| <= amax, the largest
 // vertex coordinate magnitude; then t' = lo * I - o' * I in fp32 errs by at most about
 // 6 * 2^-24 * amax in position, far inside the 2^-18 * amax the node boxes are padded by
-// (bvh.cpp), plus a relative 2^-22 in t' covered by the 2^-20 widening.  A ray that
+// (bvh.cpp), and the relative 2^-22 in t' is inside it too (RT_SLAB32_WIDEN).  A ray that
 // misses the box finds no face whatever the node tests say.  |I| is clamped to 2^60:
 // for a direction component below 2^-60 the clamped distances to the padded planes still
 // exceed any face distance (the planes lie >= 2^-18 amax from every face).
@@ -383,11 +392,14 @@ __device__ __forceinline__ bool slab32(P lo, P hi, const Ray32& r, float lim, fl
 	const float tz0 = fmaf(lo[2], r.iz, -r.oiz), tz1 = fmaf(hi[2], r.iz, -r.oiz);
 	float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
 	float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-	tmin = fmaf(-fabsf(tmin), 0x1p-20f, tmin);
-	tmax = fmaf(fabsf(tmax), 0x1p-20f, tmax);
+	if (RT_SLAB32_WIDEN) {
+		tmin = fmaf(-fabsf(tmin), 0x1p-20f, tmin);
+		tmax = fmaf(fabsf(tmax), 0x1p-20f, tmax);
+	}
 	tnear = tmin;
 	return tmax >= tmin && tmax >= 0.0f && tmin <= lim;
 }
+
 
 
 
