@@ -28,6 +28,12 @@
 // Facing pre-test (face_facing_rejects): exact skip of a face whose facing test certainly
 // fails, before its fp64 Cramer test.  0: off (A/B builds).  (A planar-geometry form, one
 // world-space dot product per geometry before its transform, measured -1.4 %: DESIGN.md.)
+#ifndef RT_FACE_ONE_FETCH
+#define RT_FACE_ONE_FETCH 1
+#endif
+#ifndef RT_NODE_PREFETCH
+#define RT_NODE_PREFETCH 1
+#endif
 #ifndef RT_FACING
 #define RT_FACING 1
 #endif
@@ -257,13 +263,14 @@ __device__ __forceinline__ bool quotient_surely_above(double num, double den, do
 // errs by < 5e-7 |c|_1, and tau = r + 2 (1e-5 max |n_i|_1 + 1e-6 |c|_1) (bvh.cpp
 // facing_data) leaves every dot(n_i, d) beyond 1e-5 |n_i|_1 with the sign of dot(c, d).
 // tau = +inf disables the face's test, a NaN compares false: never a rejection.
-template <typename FP>
-__device__ __forceinline__ bool face_facing_rejects(FP F, V3 d, bool reverse) {
-	const float s = fmaf(F->cone_c[2], static_cast<float>(d.z),
-	                     fmaf(F->cone_c[1], static_cast<float>(d.y), F->cone_c[0] * static_cast<float>(d.x)));
-	const float tau = F->cone_tau;
+__device__ __forceinline__ bool facing_rejects(float c0, float c1, float c2, float tau, V3 d, bool reverse) {
+	const float s = fmaf(c2, static_cast<float>(d.z), fmaf(c1, static_cast<float>(d.y), c0 * static_cast<float>(d.x)));
 	// s > tau: front false, rejected unless reverse; s < -tau: front true, rejected if reverse
 	return reverse ? s < -tau : s > tau;
+}
+template <typename FP>
+__device__ __forceinline__ bool face_facing_rejects(FP F, V3 d, bool reverse) {
+	return facing_rejects(F->cone_c[0], F->cone_c[1], F->cone_c[2], F->cone_tau, d, reverse);
 }
 // One iteration of the face loop of geometry.cpp:78-124.  Accepts the face when it is
 // strictly closer, or equally close with a smaller reference index: over any visiting
@@ -274,15 +281,32 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
                                           double any_limit, MeshBest& best, WorkStats& ws) {
 	ws.inc<W_TRIS>();
 	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
-	if (RT_FACING && face_facing_rejects(F, d, reverse)) return false;
-	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-	// id is fetched with the vertices: the compiler would otherwise issue its load where
-	// it is first used (one more memory round trip per candidate face)
-	const int32_t id = F->id;
-	if constexpr (kUniform)
-		asm volatile("" ::"s"(id));  // materialised here: no separate fetch at its first use
-	else
-		asm volatile("" ::"v"(id));
+	// A wave-uniform record (RT_FACE_ONE_FETCH): vertices, id and cone in one round of scalar
+	// loads before the facing pre-test, else the vertices wait for a second memory round
+	// trip after it.  Per lane, the vertices are fetched only for faces the pre-test keeps.
+	constexpr bool kEarly = kUniform && RT_FACE_ONE_FETCH;
+	V3 p0, va, vb;
+	int32_t id;
+	if constexpr (kEarly) {
+		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+		id = F->id;
+		const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
+		asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
+		             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
+		if (RT_FACING && facing_rejects(c0, c1, c2, tau, d, reverse)) return false;
+	} else if (RT_FACING && face_facing_rejects(F, d, reverse)) {
+		return false;
+	}
+	if constexpr (!kEarly) {
+		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+		// id is fetched with the vertices: the compiler would otherwise issue its load where
+		// it is first used (one more memory round trip per candidate face)
+		id = F->id;
+		if constexpr (kUniform)
+			asm volatile("" ::"s"(id));  // materialised here: no separate fetch at its first use
+		else
+			asm volatile("" ::"v"(id));
+	}
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	if (D == 0) return false;
@@ -750,14 +774,17 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			const Ray32 r32 = ray32(G, o, d, inv);
 			float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);  // changes only with best.dist
 			const auto nodes = uniform_ptr(S.nodes);
+			const int32_t fbase = uniform_i32(G->face_begin);
 			int32_t node = uniform_i32(G->bvh_root);
 			int sp = 0;
-			for (;;) {
-				PROF_BEGIN(tn);
-				// the whole 64-B record in one scalar load, both child boxes tested by every
-				// lane (a lane that is done ignores its results): one memory round trip
-				const auto N = nodes + node;
-				float box[2][2][3];  // [child][lo, hi][axis]
+			// the node record: the whole 64 B in one scalar load, both child boxes tested by
+			// every lane (a lane that is done ignores its results).  RT_NODE_PREFETCH: the
+			// next node's record is requested before the current node's leaf faces are
+			// tested, so its memory round trip overlaps theirs.
+			float box[2][2][3];  // [child][lo, hi][axis]
+			int32_t rf0, rf1, rc0, rc1;
+			auto fetch = [&](int32_t n) {
+				const auto N = nodes + n;
 #pragma unroll
 				for (int c = 0; c < 2; c++)
 #pragma unroll
@@ -765,7 +792,11 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 						box[c][0][a] = N->lo[c][a];
 						box[c][1][a] = N->hi[c][a];
 					}
-				const int32_t rf0 = N->first[0], rf1 = N->first[1], rc0 = N->count[0], rc1 = N->count[1];
+				rf0 = N->first[0], rf1 = N->first[1], rc0 = N->count[0], rc1 = N->count[1];
+			};
+			fetch(node);
+			for (;;) {
+				PROF_BEGIN(tn);
 				if (live) ws.inc<W_NODES>();
 				float tn0 = 0, tn1 = 0;
 				const bool h0 = slab32(box[0][0], box[0][1], r32, lim, tn0) && live;
@@ -773,19 +804,36 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
 				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
 				const int first = uniform_i32((2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0);
+				const int32_t f_first = uniform_i32(first ? rf1 : rf0), c_first = uniform_i32(first ? rc1 : rc0);
+				const int32_t f_second = uniform_i32(first ? rf0 : rf1), c_second = uniform_i32(first ? rc0 : rc1);
+				const bool w_first = first ? h1 : h0, w_second_box = first ? h0 : h1;
+				const float tn_second = first ? tn0 : tn1;
 				int32_t next = -1;
 				PROF_END(ws, PH_NODES, tn);
+				if (RT_NODE_PREFETCH) {
+					// inner children first: the node to visit next is known before any leaf
+					// (an inner second child is kept with the pruning limit before the first
+					// child's faces: at most one more node visit, never a different result)
+					const bool any_first = wave_any(w_first);
+					const bool any_second = wave_any(w_second_box && live && tn_second <= lim);
+					if (any_first && c_first == 0) next = f_first;
+					if (any_second && c_second == 0) {
+						if (next < 0)
+							next = f_second;
+						else if (sp < kStackDepth)
+							wstack[sp++] = f_second;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
+					}
+					if (next < 0 && sp > 0) next = uniform_i32(wstack[--sp]);
+					if (next >= 0) fetch(uniform_i32(next));
+					// leaf children, in the same order
 #pragma unroll
-				for (int k = 0; k < 2; k++) {
-					const int c = first ^ k;
-					bool want = c ? h1 : h0;
-					if (k == 1) want = want && live && (c ? tn1 : tn0) <= lim;
-					if (!wave_any(want)) continue;
-					const int32_t cf = uniform_i32(c ? rf1 : rf0), cc = uniform_i32(c ? rc1 : rc0);
-					if (cc > 0 && (RT_DIAG_SKIP & 2)) {
-					} else if (cc > 0) {
+					for (int k = 0; k < 2; k++) {
+						const int32_t cf = k ? f_second : f_first, cc = k ? c_second : c_first;
+						if (cc <= 0) continue;
+						const bool want = k ? (w_second_box && live && tn_second <= lim) : w_first;
+						if (!wave_any(want) || (RT_DIAG_SKIP & 2)) continue;
 						PROF_BEGIN(tf);
-						const int32_t f0 = G->face_begin + cf;
+						const int32_t f0 = fbase + cf;
 						for (int32_t f = f0; f < f0 + cc; f++)
 							if (want && live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
 								settled = true;
@@ -793,18 +841,40 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 							}
 						lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 						PROF_END(ws, PH_FACES, tf);
-					} else if (next < 0) {
-						next = cf;
-					} else if (sp < kStackDepth) {
-						wstack[sp++] = cf;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
 					}
+					if (!wave_any(live) || next < 0) break;
+					node = next;
+				} else {
+#pragma unroll
+					for (int k = 0; k < 2; k++) {
+						bool want = k ? (w_second_box && live && tn_second <= lim) : w_first;
+						if (!wave_any(want)) continue;
+						const int32_t cf = k ? f_second : f_first, cc = k ? c_second : c_first;
+						if (cc > 0 && (RT_DIAG_SKIP & 2)) {
+						} else if (cc > 0) {
+							PROF_BEGIN(tf);
+							const int32_t f0 = fbase + cf;
+							for (int32_t f = f0; f < f0 + cc; f++)
+								if (want && live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+									settled = true;
+									live = false;
+								}
+							lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
+							PROF_END(ws, PH_FACES, tf);
+						} else if (next < 0) {
+							next = cf;
+						} else if (sp < kStackDepth) {
+							wstack[sp++] = cf;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
+						}
+					}
+					if (!wave_any(live)) break;
+					if (next < 0) {
+						if (sp == 0) break;
+						next = uniform_i32(wstack[--sp]);
+					}
+					node = uniform_i32(next);
+					fetch(node);
 				}
-				if (!wave_any(live)) break;
-				if (next < 0) {
-					if (sp == 0) break;
-					next = uniform_i32(wstack[--sp]);
-				}
-				node = uniform_i32(next);
 			}
 		}
 	}
