@@ -31,9 +31,6 @@
 #ifndef RT_FACE_ONE_FETCH
 #define RT_FACE_ONE_FETCH 1
 #endif
-#ifndef RT_NODE_PREFETCH
-#define RT_NODE_PREFETCH 1
-#endif
 #ifndef RT_FACING
 #define RT_FACING 1
 #endif
@@ -778,9 +775,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			int32_t node = uniform_i32(G->bvh_root);
 			int sp = 0;
 			// the node record: the whole 64 B in one scalar load, both child boxes tested by
-			// every lane (a lane that is done ignores its results).  RT_NODE_PREFETCH: the
-			// next node's record is requested before the current node's leaf faces are
-			// tested, so its memory round trip overlaps theirs.
+			// every lane (a lane that is done ignores its results)
 			float box[2][2][3];  // [child][lo, hi][axis]
 			int32_t rf0, rf1, rc0, rc1;
 			auto fetch = [&](int32_t n) {
@@ -795,98 +790,72 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				rf0 = N->first[0], rf1 = N->first[1], rc0 = N->count[0], rc1 = N->count[1];
 			};
 			fetch(node);
+			// Child lane sets are wave masks (SGPRs); a lane's predicate is its bit (inverse
+			// ballot, no instruction)
 			for (;;) {
 				PROF_BEGIN(tn);
 				if (live) ws.inc<W_NODES>();
 				float tn0 = 0, tn1 = 0;
-				const bool h0 = slab32(box[0][0], box[0][1], r32, lim, tn0) && live;
-				const bool h1 = slab32(box[1][0], box[1][1], r32, lim, tn1) && live;
-				const unsigned long long m0 = __ballot(h0), m1 = __ballot(h1);
-				const unsigned long long pref1 = __ballot(h0 && h1 && tn1 < tn0);
-				const int first = uniform_i32((2 * __popcll(pref1) > __popcll(m0 & m1) || !m0) ? 1 : 0);
-				const int32_t f_first = uniform_i32(first ? rf1 : rf0), c_first = uniform_i32(first ? rc1 : rc0);
-				const int32_t f_second = uniform_i32(first ? rf0 : rf1), c_second = uniform_i32(first ? rc0 : rc1);
-				const bool w_first = first ? h1 : h0, w_second_box = first ? h0 : h1;
-				const float tn_second = first ? tn0 : tn1;
-				int32_t next = -1;
+				const bool s0 = slab32(box[0][0], box[0][1], r32, lim, tn0);
+				const bool s1 = slab32(box[1][0], box[1][1], r32, lim, tn1);
+				const unsigned long long L = __ballot(live);
+				const unsigned long long m0 = __ballot(s0) & L, m1 = __ballot(s1) & L;
+				const unsigned long long both = m0 & m1;
+				// majority near-first: child 1 first when most lanes that need both see it nearer
+				const bool first = 2 * __popcll(__ballot(tn1 < tn0) & both) > __popcll(both) || m0 == 0;
+				const int32_t f_first = first ? rf1 : rf0, c_first = first ? rc1 : rc0;
+				const int32_t f_second = first ? rf0 : rf1, c_second = first ? rc0 : rc1;
+				const unsigned long long w_first = first ? m1 : m0, w_second = first ? m0 : m1;
 				PROF_END(ws, PH_NODES, tn);
-				if (RT_NODE_PREFETCH) {
-					// inner children first: the node to visit next is known before any leaf
-					// (an inner second child is kept with the pruning limit before the first
-					// child's faces: at most one more node visit, never a different result)
-					const bool any_first = wave_any(w_first);
-					const bool any_second = wave_any(w_second_box && live && tn_second <= lim);
-					if (any_first && c_first == 0) next = f_first;
-					if (any_second && c_second == 0) {
-						if (next < 0)
-							next = f_second;
-						else if (sp < kStackDepth)
-							wstack[sp++] = f_second;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
-					}
-					if (next < 0 && sp > 0) next = uniform_i32(wstack[--sp]);
-					if (next >= 0) fetch(uniform_i32(next));
-					// leaf children, in the same order
-#pragma unroll
-					for (int k = 0; k < 2; k++) {
-						const int32_t cf = k ? f_second : f_first, cc = k ? c_second : c_first;
-						if (cc <= 0) continue;
-						const bool want = k ? (w_second_box && live && tn_second <= lim) : w_first;
-						if (!wave_any(want) || (RT_DIAG_SKIP & 2)) continue;
-						PROF_BEGIN(tf);
-						const int32_t f0 = fbase + cf;
-						for (int32_t f = f0; f < f0 + cc; f++)
-							if (want && live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
-								settled = true;
-								live = false;
-							}
-						lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
-						PROF_END(ws, PH_FACES, tf);
-					}
-					if (!wave_any(live) || next < 0) break;
-					node = next;
-				} else {
-#pragma unroll
-					for (int k = 0; k < 2; k++) {
-						bool want = k ? (w_second_box && live && tn_second <= lim) : w_first;
-						if (!wave_any(want)) continue;
-						const int32_t cf = k ? f_second : f_first, cc = k ? c_second : c_first;
-						if (cc > 0 && (RT_DIAG_SKIP & 2)) {
-						} else if (cc > 0) {
-							PROF_BEGIN(tf);
-							const int32_t f0 = fbase + cf;
-							for (int32_t f = f0; f < f0 + cc; f++)
-								if (want && live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
-									settled = true;
-									live = false;
-								}
-							lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
-							PROF_END(ws, PH_FACES, tf);
-						} else if (next < 0) {
-							next = cf;
-						} else if (sp < kStackDepth) {
-							wstack[sp++] = cf;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
-						}
-					}
-					if (!wave_any(live)) break;
-					if (next < 0) {
-						if (sp == 0) break;
-						next = uniform_i32(wstack[--sp]);
-					}
-					node = uniform_i32(next);
-					fetch(node);
+				// inner children first, so the node to visit next is known (and its record
+				// requested) before the leaf faces are tested: its memory round trip overlaps
+				// theirs.  An inner second child keeps the node test's pruning limit (at most
+				// one more node visit, never a different result).
+				int32_t next = -1;
+				if (w_first && c_first == 0) next = f_first;
+				if (w_second && c_second == 0) {
+					if (next < 0)
+						next = f_second;
+					else if (sp < kStackDepth)
+						wstack[sp++] = f_second;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
 				}
+				if (next < 0 && sp > 0) next = uniform_i32(wstack[--sp]);
+				if (next >= 0) fetch(next);
+				// leaf children, in the same order; the second is tested again against the
+				// limit the first one's faces may have lowered
+				bool tested = false;
+#pragma unroll
+				for (int k = 0; k < 2; k++) {
+					const int32_t cf = k ? f_second : f_first, cc = k ? c_second : c_first;
+					if (cc <= 0 || (RT_DIAG_SKIP & 2)) continue;
+					unsigned long long want = k ? w_second : w_first;
+					if (k == 1 && tested) want &= __ballot(live && (first ? tn0 : tn1) <= lim);
+					if (!want) continue;
+					PROF_BEGIN(tf);
+					const int32_t f0 = fbase + cf;
+					for (int32_t f = f0; f < f0 + cc; f++)
+						if (__builtin_amdgcn_inverse_ballot_w64(want) && live &&
+						    test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
+							settled = true;
+							live = false;
+						}
+					lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
+					tested = true;
+					PROF_END(ws, PH_FACES, tf);
+				}
+				if (next < 0 || !wave_any(live)) break;
 			}
 		}
 	}
 	found_dist = best.dist;
-// the reference's gate (geometry.cpp:72), evaluated only for lanes with a result (see mesh_hit)
-bool keep = on && best.face >= 0;
-if (G->gate && wave_any(keep)) {
-PROF_BEGIN(tg);
-if (keep) keep = hits_bounding_box(o, d, G->bb_min, G->bb_max);
-PROF_END(ws, PH_GATE, tg);
-if (!keep) settled = false;
-}
+	// the reference's gate (geometry.cpp:72), evaluated only for lanes with a result (see mesh_hit)
+	bool keep = on && best.face >= 0;
+	if (G->gate && wave_any(keep)) {
+		PROF_BEGIN(tg);
+		if (keep) keep = hits_bounding_box(o, d, G->bb_min, G->bb_max);
+		PROF_END(ws, PH_GATE, tg);
+		if (!keep) settled = false;
+	}
 	if (!keep) return false;
 	fh = FaceHit{best.face, best.a, best.b};
 	return true;
