@@ -207,6 +207,11 @@ struct rt_scene {
 	int64_t batch_chunk_pixels = (int64_t)1 << 22;  // RTAMD_BATCH_CHUNK: most pixels of a chunk packed from several jobs
 	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
 	int shadow_all_lights = 3;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
+	// RTAMD_DEEP_SPLIT: the first n levels after the direct ones are shaded alone, each in
+	// its own launch after the chain, before one batch of the rest (a batch's first bounce
+	// then traces its shadow rays as packets; per call like direct_levels)
+	int deep_split_single = 0;
+	int deep_split_batch = 1;
 	// measured best on C3: packets for the camera rays and their first bounce, and
 	// for the shadow rays of both (once the zero-term decision thinned the per-lane waves)
 	int packet_mask =
@@ -356,6 +361,7 @@ int32_t selected_row(const rt_render_params* p, int64_t q) {
 struct Render {
 	rt_scene* s;
 	int direct_levels = 2;  // rt_scene::direct_levels_single or _batch, for this call
+	int deep_split = 0;     // rt_scene::deep_split_single or _batch, for this call
 	rt_counters cnt{};
 	float kernel_ms = 0.f;
 	Progress* progress = nullptr;
@@ -531,8 +537,8 @@ struct Render {
 			hipStream_t q = st;
 			std::vector<int> deep;
 			for (int L = direct_levels; L < nlev; L++) deep.push_back(L);
-			for (size_t k = 0; k < deep.size() && rc == RT_OK; k += rtamd::kMaxBatch) {
-				const size_t e = std::min(deep.size(), k + rtamd::kMaxBatch);
+			for (size_t k = 0, e; k < deep.size() && rc == RT_OK; k = e) {
+				e = std::min(deep.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
 				scratch.launches[1] = scratch.launches[2] = 0;
 				rc = launch_shading_dev(ln, std::vector<int>(deep.begin() + k, deep.begin() + e), q, scratch);
 				launches[1] += scratch.launches[1];
@@ -679,8 +685,8 @@ struct Render {
 			}
 		}
 		if (more) return RT_OK;
-		for (size_t k = 0; k < ln.deferred.size(); k += rtamd::kMaxBatch) {
-			const size_t e = std::min(ln.deferred.size(), k + rtamd::kMaxBatch);
+		for (size_t k = 0, e; k < ln.deferred.size(); k = e) {
+			e = std::min(ln.deferred.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
 			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, ln.shade[3]))) return rc;
 		}
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
@@ -998,6 +1004,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
+	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
+		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
 	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);
 	if (const char* gr = std::getenv("RTAMD_GRAPH")) s->graphs = std::atoi(gr);
 	if (const char* pt = std::getenv("RTAMD_PLAN_TRUNCATE")) s->plan_truncate = std::atoi(pt);
@@ -1147,6 +1155,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	if (rc) return rc;
 	Render R{s};
 	R.direct_levels = batch ? s->direct_levels_batch : s->direct_levels_single;
+	R.deep_split = batch ? s->deep_split_batch : s->deep_split_single;
 	R.progress = progress;
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
 	// the caller's stream is joined first (its prior work, e.g. the allocation of the
