@@ -117,6 +117,7 @@ struct Plan {
 	// rays and hits of every level in the traced chunk: they size the grids only (the kernels
 	// read the actual counts and stride over them, so a difference costs time, not results)
 	std::vector<int64_t> level_n, hits;
+	std::vector<int64_t> capacity;  // the building lane's level buffer capacities (plan sharing)
 	int launches[3] = {0, 0, 0};
 	hipGraphExec_t exec = nullptr;
 };
@@ -205,6 +206,12 @@ struct rt_scene {
 	// the branches and the lanes)
 	int graphs = 2;
 	int64_t batch_chunk_pixels = (int64_t)1 << 22;  // RTAMD_BATCH_CHUNK: most pixels of a chunk packed from several jobs
+	int batch_balance = 1;                       // RTAMD_BATCH_BALANCE: equal chunks, a multiple of the lanes
+	// launch plans without graphs (RTAMD_GRAPH 2) are plain data: a lane adopts a plan another
+	// lane built (growing its level buffers to the plan's capacities) instead of tracing the
+	// chunk shape host-driven itself
+	std::vector<Plan> shared_plans;
+	int plan_share = 1;                          // RTAMD_PLAN_SHARE
 	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
 	int shadow_all_lights = 3;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// RTAMD_DEEP_SPLIT: the first n levels after the direct ones are shaded alone, each in
@@ -566,6 +573,7 @@ struct Render {
 		pl.n_levels = static_cast<int>(ln.level_n.size());
 		pl.level_n = ln.level_n;
 		for (int L = 0; L < pl.n_levels; L++) pl.hits.push_back(ln.counts_host[2 * L]);
+		for (int L = 0; L < pl.n_levels; L++) pl.capacity.push_back(ln.levels[L].lv.capacity);
 		if (s->plan_truncate && pl.n_levels > 1) pl.n_levels--;  // test hook: a plan that must miss
 		if (s->graphs == 1) {
 			hipGraph_t graph = nullptr;
@@ -580,7 +588,27 @@ struct Render {
 			if (rc) return rc;
 		}
 		ln.plans.push_back(pl);
+		if (s->graphs == 2) {
+			bool known = false;
+			for (const Plan& q : s->shared_plans) known = known || q.key == pl.key;
+			if (!known) s->shared_plans.push_back(pl);
+		}
 		return RT_OK;
+	}
+
+	// A plan of this chunk's shape built by another lane (RTAMD_GRAPH 2), made this lane's
+	// own: its level buffers grown to the plan's capacities
+	Plan* adopt_plan(Lane& ln, const PlanKey& k, int& rc) {
+		rc = RT_OK;
+		if (s->graphs != 2 || s->serial || !s->plan_share) return nullptr;
+		for (const Plan& q : s->shared_plans) {
+			if (!(q.key == k)) continue;
+			for (int L = 0; L < q.n_levels && rc == RT_OK; L++) rc = ensure_level_record(s, ln, L, q.capacity[L]);
+			if (rc) return nullptr;
+			ln.plans.push_back(q);
+			return &ln.plans.back();
+		}
+		return nullptr;
 	}
 
 	// the chunk's row table: image row and output rows of every selected row of its pieces
@@ -640,7 +668,9 @@ struct Render {
 		ln.shaded.clear();
 		ln.deferred.clear();
 		ln.planned = nullptr;
-		if (Plan* pl = find_plan(ln, key_of(ln))) {
+		Plan* pl = find_plan(ln, key_of(ln));
+		if (!pl && (pl = adopt_plan(ln, key_of(ln), rc), rc)) return rc;
+		if (pl) {
 			if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
 			if (pl->exec) {
 				HIP_TRY(hipGraphLaunch(pl->exec, ln.stream));
@@ -1010,6 +1040,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* gr = std::getenv("RTAMD_GRAPH")) s->graphs = std::atoi(gr);
 	if (const char* pt = std::getenv("RTAMD_PLAN_TRUNCATE")) s->plan_truncate = std::atoi(pt);
 	if (const char* bc = std::getenv("RTAMD_BATCH_CHUNK")) s->batch_chunk_pixels = std::max<int64_t>(1, std::atoll(bc));
+	if (const char* bb = std::getenv("RTAMD_BATCH_BALANCE")) s->batch_balance = std::atoi(bb);
+	if (const char* ps = std::getenv("RTAMD_PLAN_SHARE")) s->plan_share = std::atoi(ps);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
@@ -1130,6 +1162,7 @@ int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_coun
 		// whole call again host-driven, which sizes every level from the counts
 		reset_after_error(s);
 		for (auto& ln : s->lanes) clear_plans(*ln);
+		s->shared_plans.clear();
 		const int graphs = s->graphs;
 		s->graphs = 0;
 		if (progress) progress->done = 0;
@@ -1169,7 +1202,49 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	// batch_chunk_pixels: rows of several frames traced as one wavefront (a GPU's share of
 	// row-partitioned frames is a few rows of each frame).
 	std::vector<std::vector<Segment>> chunks;
-	{
+	// Balanced batches (RTAMD_BATCH_BALANCE): jobs of one shape that make fewer than two
+	// chunks per lane are cut into equal chunks whose number is a multiple of the lane count,
+	// so that no lane traces a last chunk alone at the end of the call (a GPU's share of
+	// row-partitioned frames); cuts fall on 8-row boundaries (whole 8x8 ray tiles).
+	int64_t bal_rows = 0;
+	if (batch && s->batch_balance) {
+		const Job& j0 = jobs.front();
+		int64_t limit_px = s->batch_chunk_pixels, total_rows = 0;
+		bool uniform = true;
+		for (const Job& job : jobs) {
+			const rt_render_params* p = job.p;
+			uniform = uniform && p->width == j0.p->width && p->height == j0.p->height && job.depth == j0.depth &&
+			          job.io == j0.io;
+			limit_px = std::min(limit_px, p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22);
+			total_rows += job.n_rows;
+		}
+		const int64_t lim_rows = (limit_px / j0.W) & ~int64_t(7);
+		const int64_t lanes = static_cast<int64_t>(n_lanes);
+		int64_t n = lim_rows >= 8 ? (total_rows + lim_rows - 1) / lim_rows : 0;
+		// only a call of few chunks is balanced: with many, the last one's tail is a small
+		// share of the call, and whole frames keep one chunk shape (one launch plan per lane)
+		if (uniform && total_rows > 0 && n > 0 && n < 2 * lanes && n % lanes != 0) {
+			n = (n + lanes - 1) / lanes * lanes;
+			bal_rows = std::min(lim_rows, ((total_rows + n - 1) / n + 7) & ~int64_t(7));
+		}
+	}
+	if (bal_rows > 0) {
+		std::vector<Segment> cur;
+		int64_t cur_rows = 0;
+		for (const Job& job : jobs)
+			for (int64_t r0 = 0; r0 < job.n_rows;) {
+				const int64_t take = std::min(job.n_rows - r0, bal_rows - cur_rows);
+				cur.push_back(Segment{&job, r0, take});
+				r0 += take;
+				cur_rows += take;
+				if (cur_rows == bal_rows) {
+					chunks.push_back(cur);
+					cur.clear();
+					cur_rows = 0;
+				}
+			}
+		if (!cur.empty()) chunks.push_back(cur);
+	} else {
 		std::vector<Segment> cur;
 		int64_t cur_px = 0, cur_limit = 0;
 		for (const Job& job : jobs) {
