@@ -1,5 +1,8 @@
 #!/bin/bash
-# usage: emu_ab.sh rounds steps warmup "e:vars" ...
+# A/B of one GPU's share of an e-way row partition (bench.py --emulate-ranks e) under
+# environment settings, round-robin on one box (GPU box, from the repo root).
+#   usage: tools/emu_ab.sh <rounds> <steps> <warmup> "<e>:<VAR=VALUE[,VAR=VALUE]>" ...
+#   e.g.   tools/emu_ab.sh 2 60 3 "8:X=1" "8:RTAMD_BATCH_BALANCE=0"
 set -o pipefail
 N=$1; ST=$2; WU=$3; shift 3
 for r in $(seq 1 $N); do
