@@ -111,6 +111,9 @@ struct PlanKey {
 	}
 };
 
+// plans kept per lane and shared per scene (oldest dropped first): a batch of one shape has
+// at most 2 x lanes chunk shapes
+constexpr size_t kMaxPlans = 64;
 struct Plan {
 	PlanKey key{};
 	int n_levels = 0;
@@ -587,13 +590,25 @@ struct Render {
 			if (graph) (void)hipGraphDestroy(graph);
 			if (rc) return rc;
 		}
-		ln.plans.push_back(pl);
+		keep_plan(ln, pl);
 		if (s->graphs == 2) {
 			bool known = false;
 			for (const Plan& q : s->shared_plans) known = known || q.key == pl.key;
-			if (!known) s->shared_plans.push_back(pl);
+			if (!known) {
+				if (s->shared_plans.size() >= kMaxPlans) s->shared_plans.erase(s->shared_plans.begin());
+				s->shared_plans.push_back(pl);
+			}
 		}
 		return RT_OK;
+	}
+
+	// a lane keeps its kMaxPlans most recent plans (called while it replays none)
+	static void keep_plan(Lane& ln, const Plan& pl) {
+		if (ln.plans.size() >= kMaxPlans) {
+			if (ln.plans.front().exec) (void)hipGraphExecDestroy(ln.plans.front().exec);
+			ln.plans.erase(ln.plans.begin());
+		}
+		ln.plans.push_back(pl);
 	}
 
 	// A plan of this chunk's shape built by another lane (RTAMD_GRAPH 2), made this lane's
@@ -605,7 +620,7 @@ struct Render {
 			if (!(q.key == k)) continue;
 			for (int L = 0; L < q.n_levels && rc == RT_OK; L++) rc = ensure_level_record(s, ln, L, q.capacity[L]);
 			if (rc) return nullptr;
-			ln.plans.push_back(q);
+			keep_plan(ln, q);
 			return &ln.plans.back();
 		}
 		return nullptr;
