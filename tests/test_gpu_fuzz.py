@@ -9,6 +9,8 @@ The image (binary64 bit patterns, NaN payloads and -0 included) and the referenc
 counters must equal the oracle's (pinned to the unmodified reference, test_oracle.py).
 The generator is seeded: a failing seed reproduces exactly.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -90,7 +92,12 @@ def random_scene(seed, tmp_path):
     return str(path), int(rng.integers(0, 7)), io
 
 
-@pytest.mark.parametrize("seed", range(256))
+# RTAMD_FUZZ_BASE / RTAMD_FUZZ_SEEDS widen the sweep for one-off runs (default: seeds 0-255)
+_BASE = int(os.environ.get("RTAMD_FUZZ_BASE", "0"))
+_SEEDS = int(os.environ.get("RTAMD_FUZZ_SEEDS", "256"))
+
+
+@pytest.mark.parametrize("seed", range(_BASE, _BASE + _SEEDS))
 def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed):
     path, bdepth, io = random_scene(seed, tmp_path)
     w, h = 56, 40
