@@ -120,3 +120,32 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed):
     diff = int((g != r).any(axis=2).sum())
     assert diff == 0, f"seed {seed}: {diff} pixels differ from the oracle"
     assert (st.trace_rays, st.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+
+
+@pytest.mark.parametrize("seed", range(1000, 1064))
+def test_random_scene_batch_partition(gpu, oracle, tmp_path, seed):
+    """Random scenes through the batch path (rt_render_batch_device, 3 lanes): the whole
+    frame and both halves of a 2-way 8-row-block partition in one call, cut into balanced
+    chunks that end inside frames, with the first bounce shaded alone (batch schedule):
+    every row equals the oracle's, bit for bit."""
+    torch = pytest.importorskip("torch")
+    path, bdepth, io = random_scene(seed, tmp_path)
+    if io:
+        pytest.skip("--intersection-only normalises over the whole frame (covered by the single-frame sweep)")
+    w, h = 56, 40
+    try:
+        want, _ = oracle.render(path, w, h, bdepth=bdepth)
+    except RuntimeError:
+        pytest.skip("the reference rejects the scene (covered by the single-frame sweep)")
+    s = gpu.load_scene(path)
+    jobs = [s.params(w, h, bdepth, False), s.params(w, h, bdepth, False, 0, h, 2, row_block=8),
+            s.params(w, h, bdepth, False, 8, h, 2, row_block=8)]
+    rows = [list(range(h)), [r for r in range(h) if (r // 8) % 2 == 0], [r for r in range(h) if (r // 8) % 2 == 1]]
+    outs = [torch.full((len(r), w, 3), -1.0, dtype=torch.float64, device="cuda") for r in rows]
+    torch.cuda.synchronize()
+    s.render_batch_device(jobs, [o.data_ptr() for o in outs], [0] * len(jobs))
+    for o, r in zip(outs, rows):
+        g = np.ascontiguousarray(o.cpu().numpy()).view(np.uint64)
+        ref = np.ascontiguousarray(want[r]).view(np.uint64)
+        assert int((g != ref).any(axis=2).sum()) == 0, f"seed {seed}"
+    s.close()
