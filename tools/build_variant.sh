@@ -3,6 +3,7 @@
 # cs184-raytracer_amd/rtamd/var/librtamd_<tag>.so (here, on the CPU; the .so travels to the
 # GPU box with the tree; load it there with RTAMD_LIB=...).  The default build is untouched.
 #   usage: tools/build_variant.sh <tag> "<defines>"      e.g. tools/build_variant.sh nobvh -DRT_DIAG_SKIP=1
+#   EXTRA_HIP="<flags>": device compiler flags for the HIP sources only (e.g. -mllvm options)
 set -e
 TAG=$1
 DEFS=$2
@@ -13,7 +14,7 @@ mkdir -p $B $P/rtamd/var
 rm -f $B/*.o
 FL="-O3 -fPIC -std=c++17 -ffp-contract=off -Wall $DEFS"
 HIPCC=/opt/rocm/bin/hipcc
-$HIPCC $FL --offload-arch=gfx950 -munsafe-fp-atomics -c -o $B/trace.o $P/csrc/trace.hip &
+$HIPCC $FL $EXTRA_HIP --offload-arch=gfx950 -munsafe-fp-atomics -c -o $B/trace.o $P/csrc/trace.hip &
 $HIPCC $FL --offload-arch=gfx950 -munsafe-fp-atomics -c -o $B/api.o $P/csrc/api.cpp &
 for f in scene_host bvh png; do
 	g++ $FL -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c -o $B/$f.o $P/csrc/$f.cpp &
