@@ -92,15 +92,17 @@ def random_scene(seed, tmp_path):
     return str(path), int(rng.integers(0, 7)), io
 
 
-# RTAMD_FUZZ_BASE / RTAMD_FUZZ_SEEDS widen the sweep for one-off runs (default: seeds 0-255)
+# RTAMD_FUZZ_BASE / RTAMD_FUZZ_SEEDS / RTAMD_FUZZ_SIZE widen the sweep for one-off runs
+# (default: seeds 0-255 at 56x40)
 _BASE = int(os.environ.get("RTAMD_FUZZ_BASE", "0"))
 _SEEDS = int(os.environ.get("RTAMD_FUZZ_SEEDS", "256"))
+_W, _H = (int(v) for v in os.environ.get("RTAMD_FUZZ_SIZE", "56x40").split("x"))  # image size of the sweep
 
 
 @pytest.mark.parametrize("seed", range(_BASE, _BASE + _SEEDS))
 def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed):
     path, bdepth, io = random_scene(seed, tmp_path)
-    w, h = 56, 40
+    w, h = _W, _H
     try:
         want, cnt = oracle.render(path, w, h, bdepth=bdepth, intersection_only=io)
     except RuntimeError as e:  # the reference rejects the scene (e.g. a vanishing direction)
