@@ -1195,21 +1195,10 @@ int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_coun
 	return rc;
 }
 
-int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
-                     Progress* progress) {
-	const bool batch = jobs.size() > 1;
-	const size_t n_lanes = batch ? std::min<size_t>(jobs.size(), s->batch_lanes) : s->single_lanes;
-	int rc = ensure_lanes(s, n_lanes);
-	if (rc) return rc;
-	Render R{s};
-	R.direct_levels = batch ? s->direct_levels_batch : s->direct_levels_single;
-	R.deep_split = batch ? s->deep_split_batch : s->deep_split_single;
-	R.progress = progress;
-	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
-	// the caller's stream is joined first (its prior work, e.g. the allocation of the
-	// output buffers, completes before ours starts); the call returns when all is done
-	HIP_TRY(hipEventRecord(s->fork_event, caller));
-	for (size_t k = 0; k < n_lanes; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k]->stream, s->fork_event, 0));
+// The chunks of a render call: every job's selected rows as segments, packed into chunks
+// (render_jobs_impl; rt_debug_plan_chunks exposes it to the CPU tests).
+std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size_t n_lanes, bool batch,
+                                              int64_t batch_chunk_pixels, int batch_balance, int chunks_per_lane) {
 	// Pieces: every job's selected rows cut into pieces of at most its chunk size (4 M
 	// pixels by default: it bounds the level buffers); one image over several lanes is cut
 	// so that every lane holds `chunks_per_lane` of its pieces.  Consecutive pieces of
@@ -1222,9 +1211,9 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	// so that no lane traces a last chunk alone at the end of the call (a GPU's share of
 	// row-partitioned frames); cuts fall on 8-row boundaries (whole 8x8 ray tiles).
 	int64_t bal_rows = 0;
-	if (batch && s->batch_balance) {
+	if (batch && batch_balance) {
 		const Job& j0 = jobs.front();
-		int64_t limit_px = s->batch_chunk_pixels, total_rows = 0;
+		int64_t limit_px = batch_chunk_pixels, total_rows = 0;
 		bool uniform = true;
 		for (const Job& job : jobs) {
 			const rt_render_params* p = job.p;
@@ -1266,7 +1255,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 			const rt_render_params* p = job.p;
 			const int64_t limit_px = p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22;
 			const int64_t max_rows = std::max<int64_t>(1, limit_px / job.W);
-			const int64_t want = (!batch && n_lanes > 1) ? static_cast<int64_t>(n_lanes) * s->chunks_per_lane : 1;
+			const int64_t want = (!batch && n_lanes > 1) ? static_cast<int64_t>(n_lanes) * chunks_per_lane : 1;
 			const int64_t piece = std::min(max_rows, std::max<int64_t>(1, (job.n_rows + want - 1) / want));
 			for (int64_t r0 = 0; r0 < job.n_rows; r0 += piece) {
 				const Segment sg{&job, r0, std::min(piece, job.n_rows - r0)};
@@ -1276,7 +1265,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 					const Job& f = *cur.front().job;
 					fits = cur.back().job != &job && f.p->width == p->width && f.p->height == p->height &&
 					       f.depth == job.depth && f.io == job.io &&
-					       cur_px + px <= std::min({cur_limit, limit_px, s->batch_chunk_pixels});
+					       cur_px + px <= std::min({cur_limit, limit_px, batch_chunk_pixels});
 				}
 				if (!fits && !cur.empty()) {
 					chunks.push_back(cur);
@@ -1290,6 +1279,26 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 		}
 		if (!cur.empty()) chunks.push_back(cur);
 	}
+	return chunks;
+}
+
+int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
+                     Progress* progress) {
+	const bool batch = jobs.size() > 1;
+	const size_t n_lanes = batch ? std::min<size_t>(jobs.size(), s->batch_lanes) : s->single_lanes;
+	int rc = ensure_lanes(s, n_lanes);
+	if (rc) return rc;
+	Render R{s};
+	R.direct_levels = batch ? s->direct_levels_batch : s->direct_levels_single;
+	R.deep_split = batch ? s->deep_split_batch : s->deep_split_single;
+	R.progress = progress;
+	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
+	// the caller's stream is joined first (its prior work, e.g. the allocation of the
+	// output buffers, completes before ours starts); the call returns when all is done
+	HIP_TRY(hipEventRecord(s->fork_event, caller));
+	for (size_t k = 0; k < n_lanes; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k]->stream, s->fork_event, 0));
+	const std::vector<std::vector<Segment>> chunks =
+	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, s->batch_balance, s->chunks_per_lane);
 	size_t next_chunk = 0;
 	for (;;) {
 		bool busy = false;
@@ -1378,6 +1387,36 @@ Job make_job(const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_d
 	j.W = p->width;
 	j.n_rows = selected_rows(p);
 	return j;
+}
+
+// CPU test hook (tests/test_host.py): the chunks a render call cuts `n` jobs into over
+// `n_lanes` lanes (rt_render_batch_device: n_lanes = min(n, batch lanes)).  Segment k of
+// the plan is out[4k..4k+3] = (chunk, job index in params, first row ordinal, rows); returns
+// the number of segments, or -1 when out_cap segments do not suffice.  Needs no device.
+extern "C" int rt_debug_plan_chunks(int n, const rt_render_params* params, int n_lanes, int64_t batch_chunk_pixels,
+                                    int balance, int64_t* out, int out_cap) {
+	std::vector<Job> jobs;
+	std::vector<int> index;
+	for (int k = 0; k < n; k++) {
+		const Job j = make_job(params + k, nullptr, nullptr);
+		if (j.n_rows <= 0) continue;
+		jobs.push_back(j);
+		index.push_back(k);
+	}
+	if (jobs.empty()) return 0;
+	const auto chunks = plan_chunks(jobs, static_cast<size_t>(std::max(1, n_lanes)), jobs.size() > 1,
+	                                batch_chunk_pixels, balance, 2);
+	int q = 0;
+	for (size_t c = 0; c < chunks.size(); c++)
+		for (const Segment& sg : chunks[c]) {
+			if (q >= out_cap) return -1;
+			out[4 * q] = static_cast<int64_t>(c);
+			out[4 * q + 1] = index[sg.job - jobs.data()];
+			out[4 * q + 2] = sg.r0;
+			out[4 * q + 3] = sg.rows;
+			q++;
+		}
+	return q;
 }
 
 void add_counters(rt_counters& a, const rt_counters& b) {

@@ -145,3 +145,71 @@ def test_libm_pow_identities_used_by_shading():
         assert m.pow(x, 1.0) == x
         assert m.pow(x, -0.0) == 1.0 and m.pow(x, 0.0) == 1.0
     assert np.isnan(m.pow(float("nan"), 1.0)) and m.pow(float("nan"), -0.0) == 1.0
+
+
+def _plan(rt, params, lanes, chunk=1 << 22, balance=1):
+    """rt_debug_plan_chunks: [(chunk, job, r0, rows)] of a render call (no device needed)."""
+    import ctypes
+    L = rt.lib()
+    f = L.rt_debug_plan_chunks
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    arr = (rt.rt_render_params * len(params))(*params)
+    out = (ctypes.c_int64 * (4 * 100000))()
+    q = f(len(params), ctypes.cast(arr, ctypes.c_void_p), lanes, chunk, balance, out, 100000)
+    assert q >= 0
+    return [tuple(out[4 * k:4 * k + 4]) for k in range(q)]
+
+
+def _rows(p):
+    from rtamd import dist as rd
+    if p.row_block > 1:
+        return rd.n_rows(p.height, p.row_begin // p.row_block, p.row_step, p.row_block)
+    return len(range(p.row_begin, p.row_end, p.row_step))
+
+
+@pytest.mark.parametrize("frames,ways,lanes", [(32, 1, 3), (32, 2, 3), (32, 4, 3), (32, 8, 3), (7, 1, 2), (5, 4, 3),
+                                               (1, 1, 1), (3, 8, 3)])
+def test_chunk_plan_covers_every_row_once(rt, frames, ways, lanes):
+    """The chunk plan of a batch (render_jobs: packed and balanced chunks) covers every
+    selected row of every frame exactly once, in order; a chunk holds at most one segment
+    per frame and at most 4 M pixels; a balanced plan (fewer than two chunks per lane
+    unbalanced) has a multiple of the lanes of chunks, cut on 8-row boundaries."""
+    W, H = 1920, 1080
+    mk = lambda: rt.rt_render_params(W, H, 4, 0, 0, H, 1, 0, 1, 0) if ways == 1 else \
+        rt.rt_render_params(W, H, 4, 0, 8 * (ways - 1), H, ways, 0, 8, 0)  # the last rank's share
+    params = [mk() for _ in range(frames)]
+    plan = _plan(rt, params, lanes)
+    for j, p in enumerate(params):
+        segs = [(r0, n) for c, jj, r0, n in plan if jj == j]
+        nxt = 0
+        for r0, n in segs:
+            assert r0 == nxt and n > 0
+            nxt += n
+        assert nxt == _rows(p)
+    chunks = sorted({c for c, *_ in plan})
+    assert chunks == list(range(len(chunks)))
+    for c in chunks:
+        segs = [s for s in plan if s[0] == c]
+        assert len({s[1] for s in segs}) == len(segs)
+        assert sum(s[3] for s in segs) * W <= 1 << 22
+    total = sum(_rows(p) for p in params)
+    lim = (1 << 22) // W // 8 * 8
+    unbalanced = -(-total // lim)
+    if frames > 1 and unbalanced < 2 * lanes and unbalanced % lanes:
+        n = -(-unbalanced // lanes) * lanes                # a multiple of the lanes
+        rows = min(lim, (-(-total // n) + 7) // 8 * 8)     # equal chunks, 8-row cuts
+        assert len(chunks) == -(-total // rows) and len(chunks) <= n
+        for c in chunks[:-1]:
+            assert sum(s[3] for s in plan if s[0] == c) == rows
+
+
+def test_chunk_plan_unbalanced_whole_frames(rt):
+    """Whole frames of a 32-frame step keep their two-frame chunks (16 of them: many chunks
+    per lane, so no balancing) and the balancing switch changes nothing there."""
+    W, H = 1920, 1080
+    params = [rt.rt_render_params(W, H, 4, 0, 0, H, 1, 0, 1, 0) for _ in range(32)]
+    a, b = _plan(rt, params, 3, balance=1), _plan(rt, params, 3, balance=0)
+    assert a == b
+    assert len({c for c, *_ in a}) == 16 and all(n == H for *_, n in a)
