@@ -126,6 +126,46 @@ def _cores():
     return max(1, min(16, n))  # the GPU box's CPU share is 16
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def reference_single_thread(s, scene, w, h, bdepth, target_s):
+    """The unmodified reference on ONE core (one worker process, SURVEY.md §8d asks for the
+    single-thread time beside the many-core one): evenly spaced rows of the same frame until
+    about target_s of CPU work; rays are the kernels' counts for the same rows."""
+    import subprocess
+    import rtamd
+    harness = os.path.join(REPO, "oracle", "_ref", "refharness")
+    if not os.access(harness, os.X_OK):
+        return None
+    step = 270
+    while True:
+        rows = (step // 2, h, step)
+        env = dict(os.environ, RT_REF_ROWS="%d:%d:%d" % rows)
+        t0 = time.perf_counter()
+        subprocess.run([harness, scene, "-o", "/dev/null", "-w", str(w), "-h", str(h), "--bdepth", str(bdepth),
+                        "-t", "1"], env=env, check=True, capture_output=True)
+        dt = time.perf_counter() - t0
+        if dt * 2.5 > target_s or step <= 1:
+            s.renderScene(options=rtamd.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth), rows=rows)
+            rays = s.last_stats.rays
+            n = len(range(*rows))
+            return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "reference",
+                    "sample": f"unmodified reference (oracle/_ref/refharness -t 1), {n} rows (every {step}th) of "
+                              f"the same {w}x{h} frame: {rays} rays in {dt:.2f} s wall (incl. scene parse)",
+                    "frame_s_projected": round(dt * h / n, 1)}
+        step = max(1, int(step / max(2.0, min(8.0, target_s / max(dt, 1e-3) / 1.5))))
+
+
 def cpu_baseline(s, scene, w, h, bdepth, target_s):
     """CPU leg on this host's cores over a bounded, evenly spaced row sample of the same frame.
 
@@ -185,6 +225,30 @@ def same_algorithm_baseline(scene, w, h, bdepth, target_s):
     return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"same-algorithm CPU port (oracle/cpu_bvh_cli, {cores} threads: LBVH, any-hit shadows, "
                       f"zero-term decisions), {runs} whole {w}x{h} frames: {rays} rays in {secs:.1f} s of render time"}
+
+
+def frame_parity(cfg, frame8, frame64):
+    """The headline's images against the unmodified reference (tests/golden/ref_hashes.json,
+    generated by tests/golden/make_golden.py from oracle/_ref): sha256 of one RGB8 frame of
+    the last timed step (and of its f64 image when this rank rendered whole frames).
+    Reference output contract: scene.cpp:25-31 (RasterImage), writers.cpp:4-9 (RGB8)."""
+    import hashlib
+    try:
+        ref = json.load(open(os.path.join(REPO, "tests", "golden", "ref_hashes.json")))["configs"][cfg]
+    except (OSError, ValueError, KeyError):
+        return {"parity": None, "note": "no golden hashes for " + cfg}
+    out = {"golden": "tests/golden/ref_hashes.json configs." + cfg}
+    ok = True
+    if frame8 is not None:
+        got = hashlib.sha256(frame8.contiguous().cpu().numpy().tobytes()).hexdigest()
+        out["rgb8_sha256_match"] = got == ref["rgb8_sha256"]
+        ok = ok and out["rgb8_sha256_match"]
+    if frame64 is not None:
+        got = hashlib.sha256(frame64.contiguous().cpu().numpy().tobytes()).hexdigest()
+        out["f64_sha256_match"] = got == ref["f64_sha256"]
+        ok = ok and out["f64_sha256_match"]
+    out["parity"] = bool(ok) if (frame8 is not None or frame64 is not None) else None
+    return out
 
 
 def stage_work(st):
@@ -293,15 +357,72 @@ def roofline(solo, frames, traffic_path, concurrent, valu_path=None):
                      "stream; rocprofv3 of `bench.py --solo-only` gives the same durations (profiles/)",
         "avg_launch_ms": round(t_launch_s * 1e3, 4), "launches_per_frame": launches / frames,
         "algorithmic_bytes_per_launch": round(alg_bytes), "fp64_flops_per_launch": round(flops),
-        "hbm_algorithmic": {"achieved": round(alg_bytes / t_launch_s / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": round(alg_bytes / t_launch_s / 1e9 / HBM_PEAK_GBS, 4),
-                            "note": "the contract's reading (algorithmic bytes vs HBM); the scene reads are "
-                                    "served on die, so `hbm` (PMC bytes) is the HBM figure"},
         "roofs": roofs, "traffic_source": traffic_note,
         "solo_ms_per_frame": {STAGES[k]: round(solo["ms"][k] / frames, 4) for k in range(3)},
         "solo_frame_wall_ms": round(solo["wall"] / frames * 1e3, 3),
         "concurrent": concurrent,
     }
+
+
+XGMI_LINK_GBS = 64.0    # assumed per-link, per-direction rate of the RGB8 gather (prompt: 7 links x ~153 GB/s per GPU)
+XGMI_FIXED_US = 25.0    # assumed fixed cost of one RCCL gather
+
+
+def emulated_scaling(a, local, torch):
+    """Single-frame strong scaling emulated on ONE GPU (WORLD_SIZE=1): for n = 1, 2, 4, 8, every
+    rank's share of ONE frame (8-row blocks interleaved, rank k: rows (r // 8) mod n == k; the
+    reference's block dispenser scene.cpp:13-48 at GPU granularity) is rendered alone, one share
+    at a time, on this GPU.  Reported per n: each share's render ms (median of reps), the max
+    (an n-GPU frame waits for its slowest rank), the imbalance (max / mean) and a projected
+    speed-up = T(1) / (max share + gather), the gather priced at the RGB8 rows of the largest
+    remote share over one xGMI link at an ASSUMED rate (XGMI_LINK_GBS, XGMI_FIXED_US): every
+    remote rank sends to rank 0 over its own link."""
+    import rtamd
+    from rtamd import dist as rd
+    from rtamd.configs import CONFIGS, SCENES, option_kwargs
+    out = {}
+    blk = max(1, a.row_block)
+    stream = torch.cuda.current_stream().cuda_stream
+    for cfg in [c for c in a.sweep.split(",") if c]:
+        scene_rel, W, H, flags = CONFIGS[cfg]
+        kw = option_kwargs(flags)
+        s = rtamd.load_scene(os.path.join(SCENES, scene_rel), device=local)
+        s.upload()
+        curve = []
+        for n in (1, 2, 4, 8):
+            n_max = max(rd.n_rows(H, k, n, blk) for k in range(n))
+            buf = torch.zeros((n_max, W, 3), dtype=torch.uint8, device="cuda")
+            share_ms, rays = [], 0
+            for k in range(n):
+                prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], k * blk, H, n, row_block=blk)
+                ts = []
+                for rep in range(a.sweep_reps + 1):  # rep 0: warm-up (level buffers, launch plans)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    st = s.render_device(prm, 0, buf.data_ptr(), stream)
+                    torch.cuda.synchronize()
+                    if rep > 0:
+                        ts.append(time.perf_counter() - t0)
+                share_ms.append(statistics.median(ts) * 1e3)
+                rays += st.rays
+            remote_rows = max([rd.n_rows(H, k, n, blk) for k in range(1, n)] or [0])
+            gather_ms = 0.0 if n == 1 else (remote_rows * W * 3 / (XGMI_LINK_GBS * 1e9) * 1e3 + XGMI_FIXED_US / 1e3)
+            proj = max(share_ms) + gather_ms
+            curve.append({"n_gpus": n, "render_ms_per_rank": [round(x, 3) for x in share_ms],
+                          "max_ms": round(max(share_ms), 3), "imbalance": round(max(share_ms) / (sum(share_ms) / n), 3),
+                          "gather_ms_assumed": round(gather_ms, 4), "projected_ms": round(proj, 3), "rays": int(rays)})
+        base = curve[0]["projected_ms"]
+        for r in curve:
+            r["projected_speedup"] = round(base / r["projected_ms"], 3)
+            r["projected_efficiency"] = round(base / r["projected_ms"] / r["n_gpus"], 3)
+        out[cfg] = {"emulated": True, "scene": scene_rel, "width": W, "height": H, "bounce_depth": kw["bdepth"],
+                    "partition": f"{blk}-row blocks interleaved (row r -> rank (r // {blk}) mod n); each rank's share "
+                                 "rendered alone on this one GPU, one share at a time",
+                    "gather_model": f"largest remote share's RGB8 rows / {XGMI_LINK_GBS:g} GB/s per xGMI link + "
+                                    f"{XGMI_FIXED_US:g} us (assumed, not measured)",
+                    "curve": curve}
+        s.close()
+    return out
 
 
 def strong_scaling(a, world, rank, local, groups, dist, torch):
@@ -499,6 +620,15 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the timed path's own output, checked against the reference (after the timed region):
+    # rank 0's assembled RGB8 frame of the last step, and its f64 image when it rendered whole frames
+    parity = None
+    if rank == 0 and ways == world:
+        last = (n_steps[0] - 1) % 2
+        f8 = frames[n_frames_rank0 - 1] if frames is not None else None
+        f64 = outs[B - 1] if (not partition or world == 1) else None
+        parity = frame_parity(a.config, f8, f64)
+        parity["frame"] = f"frame {n_frames_rank0 - 1} of the last timed step (buffer set {last})"
     # wall-clock of ONE frame's rows on this rank (one render call, nothing else in flight)
     lat = []
     for _ in range(max(0, a.latency_frames)):
@@ -533,7 +663,9 @@ def main():
         with stdout_to_stderr():
             groups.append((n, dist.new_group(list(range(n))) if world > 1 and n > 1 else None))
         n *= 2
-    if a.sweep:
+    if a.sweep and world == 1 and a.emulate_ranks <= 1:
+        sweep = emulated_scaling(a, local, torch)
+    elif a.sweep:
         sweep = strong_scaling(a, world, rank, local, groups, dist, torch)
     solo = solo_pass(scene, W, H, kw, a.solo_frames, local) if rank == 0 and a.solo_frames > 0 else None
 
@@ -572,6 +704,7 @@ def main():
             "per_rank": {"ms_per_step": [round(x, 3) for x in rank_ms],
                          "imbalance": round(max(rank_ms) / (sum(rank_ms) / len(rank_ms)), 3)},
             "roofline": roofline(solo, a.solo_frames, traffic_path, concurrent, latest_valu()) if solo else None,
+            "parity": parity,
             "work_per_frame_rank0": work,
             "strong_scaling": sweep,
         }
@@ -581,6 +714,10 @@ def main():
             res["roofline"]["solo_ms_per_step"] = round(res["roofline"]["solo_ms_per_frame"][dom] * fps / world, 3)
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(s, scene, W, H, kw["bdepth"], a.cpu_seconds)
+            res["cpu_baseline"]["cpu_model"] = cpu_model()
+            one = reference_single_thread(s, scene, W, H, kw["bdepth"], a.cpu_seconds / 3)
+            if one:
+                res["cpu_baseline"]["single_thread"] = one
             same = same_algorithm_baseline(scene, W, H, kw["bdepth"], a.cpu_seconds / 3)
             if same:
                 res["cpu_baseline"]["same_algorithm"] = same

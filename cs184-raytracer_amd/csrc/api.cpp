@@ -12,6 +12,7 @@
 #include <vector>
 #include "../../include/rtamd.h"
 #include "bvh.h"
+#include "markers.h"
 #include "scene_host.h"
 #include "trace.h"
 #include "xform.h"
@@ -103,11 +104,13 @@ struct LevelBuffers {
 struct PlanKey {
 	int32_t width, height, depth, io;
 	int32_t direct_levels;  // the schedule's split of direct and batched shading (a graph bakes it in)
+	int32_t deep_split;     // levels shaded alone after the chain (per call: single frame or batch)
 	int64_t n0;
 	uint64_t rows_hash;  // the chunk's image rows (they decide the level counts)
 	bool operator==(const PlanKey& o) const {
 		return width == o.width && height == o.height && depth == o.depth && io == o.io &&
-		       direct_levels == o.direct_levels && n0 == o.n0 && rows_hash == o.rows_hash;
+		       direct_levels == o.direct_levels && deep_split == o.deep_split && n0 == o.n0 &&
+		       rows_hash == o.rows_hash;
 	}
 };
 
@@ -338,6 +341,9 @@ int lane_create(Lane& ln, int prio_low, int prio_high) {
 	HIP_TRY(hipStreamCreateWithPriority(&ln.readback, hipStreamNonBlocking, prio_high));
 	for (hipStream_t& q : ln.shade) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
 	HIP_TRY(hipEventCreateWithFlags(&ln.chunk_done, hipEventDisableTiming));
+	roctxNameHipStream("rtamd lane: k_closest chain", ln.stream);
+	roctxNameHipStream("rtamd lane: level counts read-back", ln.readback);
+	for (hipStream_t q : ln.shade) roctxNameHipStream("rtamd lane: shading", q);
 	return RT_OK;
 }
 
@@ -446,6 +452,7 @@ struct Render {
 		k.depth = ln.depth;
 		k.io = ln.io;
 		k.direct_levels = direct_levels;
+		k.deep_split = deep_split;
 		k.n0 = ln.n0;
 		k.rows_hash = ln.rows_hash;
 		return k;
@@ -1029,6 +1036,7 @@ int rt_builder_set_desc(rt_builder* b, const rt_scene_desc* d) {
 }
 
 int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
+	rtamd::MarkerRange mr("rtamd: scene LBVH build + upload");
 	*out = nullptr;
 	if (!scene.has_camera) return fail(RT_ERR_ARG, "At least one camera must be specified.");
 	int ndev = 0;
@@ -1300,6 +1308,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	const std::vector<std::vector<Segment>> chunks =
 	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, s->batch_balance, s->chunks_per_lane);
 	size_t next_chunk = 0;
+	std::unique_ptr<rtamd::MarkerRange> trace_range(new rtamd::MarkerRange("rtamd: trace (levels, shading, output)"));
 	for (;;) {
 		bool busy = false;
 		for (size_t k = 0; k < n_lanes; k++) {
@@ -1327,6 +1336,8 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 		}
 		if (!busy) break;
 	}
+	trace_range.reset();
+	rtamd::MarkerRange stats_range("rtamd: statistics read-back");
 	// all lanes' work is complete (their events were observed): reduce the statistics on the
 	// device and read back one small summary
 	HIP_TRY(rtamd::launch_stats_finish(s->stats, s->ctr, s->summary, caller));
@@ -1368,6 +1379,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 		}
 		// full-image --intersection-only: normalise in place (scene.cpp:50-58)
 		if (p->row_begin == 0 && p->row_end == p->height && p->row_step == 1 && job.out_rgb_dev) {
+			rtamd::MarkerRange nr("rtamd: --intersection-only normalisation");
 			HIP_TRY(rtamd::launch_normalize(job.n_rows * job.W * 3, job.out_rgb_dev, cnt.intersection_max,
 			                                job.out_rgb8_dev, caller));
 			HIP_TRY(hipStreamSynchronize(caller));
@@ -1541,6 +1553,7 @@ int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint
 	uint8_t* rgb8_dev = out_rgb8 ? s->out8_dev : nullptr;
 	rc = render_batch(s, 1, p, &rgb_dev, &rgb8_dev, nullptr, counters, &pr);
 	if (rc) return rc;
+	rtamd::MarkerRange cr("rtamd: image to host (PCIe)");
 	if (out_rgb) HIP_TRY(hipMemcpy(out_rgb, s->out_dev, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
 	if (out_rgb8) HIP_TRY(hipMemcpy(out_rgb8, s->out8_dev, n * 3, hipMemcpyDeviceToHost));
 	if (progress) progress(pr.total, pr.total, user);
@@ -1593,6 +1606,7 @@ void rt_partition_row(int64_t row, int n_devices, int row_block, int* device, in
 
 int rt_write_png(const char* path, const uint8_t* rgb, int width, int height) {
 	if (!path || !rgb || width <= 0 || height <= 0) return fail(RT_ERR_ARG, "bad PNG arguments");
+	rtamd::MarkerRange mr("rtamd: PNG encode + write");
 	std::vector<uint8_t> bytes;
 	int rc = rt_encode_png(rgb, width, height, &bytes);
 	if (rc) return fail(rc, "zlib failure");

@@ -3,13 +3,16 @@
 // --bdepth, --intersection-only, positional .rti files), same messages and exit codes,
 // byte-identical PNG.  Adds --device N (HIP device), --dump-raw FILE (f64 image) and
 // --gpus N (devices --device .. --device+N-1 of this node, rows in --row-block blocks
-// interleaved over them, gathered over RCCL: include/rtamd_multi.h).
+// interleaved over them, gathered over RCCL: include/rtamd_multi.h) and --devices LIST
+// (an explicit comma-separated device list for that path; a repeated device makes
+// partitions sharing one GPU).
 // The render itself runs on the GPU through the C-ABI (include/rtamd.h).
 #include <getopt.h>
 #include <signal.h>
 #include <sys/time.h>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <fstream>
 #include <iostream>
 #include <stdexcept>
@@ -25,10 +28,11 @@ struct Options {  // options.h:10-16 defaults
 	std::string output, dump_raw;
 	int threads = 1, width = 500, height = 500, bdepth = 10, device = 0;
 	int gpus = 0, row_block = 8;  // gpus 0: the single-device path
+	std::vector<int> devices;     // --devices: explicit list for the multi-device path
 	bool intersection_only = false;
 };
 
-enum { OPT_HELP = 0, OPT_BDEPTH = 256, OPT_IO, OPT_DEVICE, OPT_DUMP, OPT_GPUS, OPT_ROW_BLOCK };
+enum { OPT_HELP = 0, OPT_BDEPTH = 256, OPT_IO, OPT_DEVICE, OPT_DUMP, OPT_GPUS, OPT_ROW_BLOCK, OPT_DEVICES };
 
 bool parse_int(const char* s, int& out) {
 	try {
@@ -46,7 +50,7 @@ bool parse_command_line(int argc, char** argv, Options& o) {  // options.cpp:18-
 	                                     {"intersection-only", 0, nullptr, OPT_IO},
 	                                     {"device", 1, nullptr, OPT_DEVICE}, {"dump-raw", 1, nullptr, OPT_DUMP},
 	                                     {"gpus", 1, nullptr, OPT_GPUS},     {"row-block", 1, nullptr, OPT_ROW_BLOCK},
-	                                     {nullptr, 0, nullptr, 0}};
+	                                     {"devices", 1, nullptr, OPT_DEVICES}, {nullptr, 0, nullptr, 0}};
 	int c;
 	while ((c = getopt_long(argc, argv, "t:w:h:o:", opts, nullptr)) != -1) {
 		switch (c) {
@@ -98,6 +102,23 @@ bool parse_command_line(int argc, char** argv, Options& o) {  // options.cpp:18-
 					return false;
 				}
 				break;
+			case OPT_DEVICES: {
+				o.devices.clear();
+				std::string list = optarg;
+				size_t pos = 0;
+				while (pos <= list.size()) {
+					const size_t e = std::min(list.find(',', pos), list.size());
+					int d = -1;
+					if (!parse_int(list.substr(pos, e - pos).c_str(), d) || d < 0) {
+						std::cerr << "Error: Device list is invalid." << std::endl;
+						return false;
+					}
+					o.devices.push_back(d);
+					pos = e + 1;
+				}
+				o.gpus = static_cast<int>(o.devices.size());
+				break;
+			}
 			case OPT_ROW_BLOCK:
 				if (!parse_int(optarg, o.row_block) || o.row_block < 1) {
 					std::cerr << "Error: Row block is invalid." << std::endl;
@@ -170,8 +191,9 @@ int main(int argc, char** argv) {
 	rt_scene* scene = nullptr;
 	rt_multi* multi = nullptr;
 	if (o.gpus > 0) {
-		std::vector<int> devices;
-		for (int k = 0; k < o.gpus; k++) devices.push_back(o.device + k);
+		std::vector<int> devices = o.devices;
+		if (devices.empty())
+			for (int k = 0; k < o.gpus; k++) devices.push_back(o.device + k);
 		if (rt_multi_create(b, o.gpus, devices.data(), o.row_block, &multi)) {
 			std::cerr << "Error: " << rt_last_error() << std::endl;
 			return 1;

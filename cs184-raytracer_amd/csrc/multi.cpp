@@ -3,16 +3,24 @@
 // librtamd (one host thread per device: rt_render_device blocks); the rows then go to the
 // first device over RCCL (ncclSend/ncclRecv in one group, xGMI) and are de-interleaved
 // there (k_deinterleave, trace.hip); --intersection-only all-reduces the maxima first.
+// A device list that names one GPU more than once (several partitions sharing a GPU: the
+// N > 1 path rehearsed on one device) cannot have an RCCL communicator (one rank per GPU):
+// the rows then go to the first partition with device copies and the maxima are reduced on
+// the host; everything else (row partition, per-partition normalisation, de-interleave) is
+// the same code.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <cstring>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
 #include "../../include/rtamd.h"
 #include "../../include/rtamd_multi.h"
+#include "markers.h"
 #include "trace.h"
 
 namespace rtamd {
@@ -72,6 +80,7 @@ struct rt_multi {
 	uint8_t* img = nullptr;       // device 0: the assembled image (bytes)
 	int64_t img_cap = 0;
 	double gather_ms = 0;
+	bool rccl = true;             // distinct devices: RCCL; a shared device: copies (see top)
 };
 
 namespace {
@@ -89,6 +98,8 @@ int multi_init(rt_multi* m, int n, const int* devices, int row_block, const rt_b
 		HIP_TRY(hipStreamCreateWithFlags(&D.stream, hipStreamNonBlocking));
 		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&D.maxv), sizeof(double)));
 	}
+	m->rccl = std::set<int>(devices, devices + n).size() == static_cast<size_t>(n);
+	if (!m->rccl) return RT_OK;
 	std::vector<ncclComm_t> comms(n);
 	NCCL_TRY(ncclCommInitAll(comms.data(), n, devices));
 	for (int i = 0; i < n; i++) m->dev[i].comm = comms[i];
@@ -190,6 +201,7 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_rgb, uin
 		if (want64 && (rc = ensure(&D.f64, &D.f64_cap, rows[i] * W * 3))) return rc;
 		if (out_rgb8 && (rc = ensure(&D.u8, &D.u8_cap, rows[i] * W * 3))) return rc;
 	}
+	std::unique_ptr<rtamd::MarkerRange> phase(new rtamd::MarkerRange("rtamd_multi: devices render their row blocks"));
 	std::vector<std::thread> th;
 	for (int i = 0; i < n; i++)
 		th.emplace_back([&, i]() {
@@ -212,32 +224,49 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_rgb, uin
 	for (std::thread& t : th) t.join();
 	for (int i = 0; i < n; i++)
 		if (rcs[i]) return fail(rcs[i], errs[i]);
+	phase.reset(new rtamd::MarkerRange("rtamd_multi: max all-reduce + row gather + assembly"));
 	const double tg = now_ms();
 	// 2. --intersection-only: the global maximum (scene.cpp:50-58), then normalise on every device
 	double gmax = 0.0;
 	if (io) {
-		double mx = 2.2250738585072014e-308;  // max initialised with DBL_MIN (scene.cpp:51)
-		NCCL_TRY(ncclGroupStart());
-		for (int i = 0; i < n; i++) {
-			Device& D = m->dev[i];
-			const double v = rows[i] ? std::max(cnt[i].intersection_max, mx) : mx;
-			HIP_TRY(hipSetDevice(D.id));
-			HIP_TRY(hipMemcpyAsync(D.maxv, &v, sizeof(double), hipMemcpyHostToDevice, D.stream));
-			NCCL_TRY(ncclAllReduce(D.maxv, D.maxv, 1, ncclFloat64, ncclMax, D.comm, D.stream));
+		// max initialised with DBL_MIN (scene.cpp:51); a device without rows contributes it
+		std::vector<double> local(n, 2.2250738585072014e-308);
+		for (int i = 0; i < n; i++)
+			if (rows[i]) local[i] = std::max(cnt[i].intersection_max, local[i]);
+		if (m->rccl) {
+			// the local maxima reach the devices before the group (the renders have returned,
+			// so a synchronous copy orders nothing else)
+			for (int i = 0; i < n; i++) {
+				HIP_TRY(hipSetDevice(m->dev[i].id));
+				HIP_TRY(hipMemcpy(m->dev[i].maxv, &local[i], sizeof(double), hipMemcpyHostToDevice));
+			}
+			NCCL_TRY(ncclGroupStart());
+			for (int i = 0; i < n; i++) {
+				Device& D = m->dev[i];
+				NCCL_TRY(ncclAllReduce(D.maxv, D.maxv, 1, ncclFloat64, ncclMax, D.comm, D.stream));
+			}
+			NCCL_TRY(ncclGroupEnd());
+			for (int i = 0; i < n; i++) {
+				Device& D = m->dev[i];
+				HIP_TRY(hipSetDevice(D.id));
+				HIP_TRY(hipStreamSynchronize(D.stream));
+				HIP_TRY(hipMemcpy(&local[i], D.maxv, sizeof(double), hipMemcpyDeviceToHost));
+			}
+		} else {
+			const double g = *std::max_element(local.begin(), local.end());
+			std::fill(local.begin(), local.end(), g);
 		}
-		NCCL_TRY(ncclGroupEnd());
+		// a device's share is normalised by rt_render_device itself only when it is the whole
+		// image (n == 1: row_step 1); with n > 1 every share holds raw 1/d^2 values, even one
+		// that holds every row (H <= row_block)
 		for (int i = 0; i < n; i++) {
 			Device& D = m->dev[i];
 			HIP_TRY(hipSetDevice(D.id));
-			double g = 0;
-			HIP_TRY(hipMemcpyAsync(&g, D.maxv, sizeof(double), hipMemcpyDeviceToHost, D.stream));
-			HIP_TRY(hipStreamSynchronize(D.stream));
-			if (i == 0) mx = g;
-			if (rows[i] && rows[i] < H &&
-			    rt_normalize_device(D.scene, D.f64, rows[i] * W, g, out_rgb8 ? D.u8 : nullptr, D.stream) != RT_OK)
+			if (rows[i] && n > 1 &&
+			    rt_normalize_device(D.scene, D.f64, rows[i] * W, local[i], out_rgb8 ? D.u8 : nullptr, D.stream) != RT_OK)
 				return RT_ERR_DEVICE;
 		}
-		gmax = mx;
+		gmax = local[0];
 	}
 	// 3. rows to device 0 (one group of sends/receives: RCCL over xGMI)
 	Device& D0 = m->dev[0];
@@ -247,7 +276,18 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_rgb, uin
 		if (out_rgb && (rc = ensure(&m->dev[i].recv64, &m->dev[i].recv64_cap, rows[i] * W * 3))) return rc;
 		if (out_rgb8 && (rc = ensure(&m->dev[i].recv8, &m->dev[i].recv8_cap, rows[i] * W * 3))) return rc;
 	}
-	if (n > 1) {
+	if (n > 1 && !m->rccl) {
+		// partitions sharing a GPU: device copies into the first partition's buffers (the
+		// renders and normalisations above have completed)
+		for (int i = 1; i < n; i++) {
+			Device& D = m->dev[i];
+			if (!rows[i]) continue;
+			const size_t c = static_cast<size_t>(rows[i] * W * 3);
+			if (out_rgb)
+				HIP_TRY(hipMemcpyPeerAsync(D.recv64, D0.id, D.f64, D.id, c * sizeof(double), D0.stream));
+			if (out_rgb8) HIP_TRY(hipMemcpyPeerAsync(D.recv8, D0.id, D.u8, D.id, c, D0.stream));
+		}
+	} else if (n > 1) {
 		NCCL_TRY(ncclGroupStart());
 		for (int i = 1; i < n; i++) {
 			Device& D = m->dev[i];

@@ -175,12 +175,14 @@ def render_frame(render_rows: Callable[[Tuple[int, int, int, int]], Tuple[torch.
     """Distributed Scene::renderScene: returns the (H, W, 3) float64 frame on `dst`.
 
     render_rows(rows) renders this rank's rows (begin, end, step, block) and returns
-    (float64 (n_local, W, 3), local max).
+    (float64 (n_local, W, 3), local max).  As rt_render/rt_render_device do, it returns
+    --intersection-only values raw for a share of the rows and normalised for the whole
+    image: one rank (world 1) selects every row, so its image is already final.
     """
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     img, local_max = render_rows(rank_rows(height, rank, world, block=block))
-    if intersection_only:
+    if intersection_only and world > 1:
         m = global_max(max(local_max, 2.2250738585072014e-308), device)  # max init DBL_MIN (scene.cpp:51)
         img.mul_(1.0 / m)  # Color3d /= scalar multiplies by the reciprocal
     return gather_rows(img, height, dst, block=block)

@@ -15,7 +15,10 @@
  *   --intersection-only global max (scene.cpp:50-58)   ncclAllReduce(MAX) of the devices'
  *                                                        maxima, then each device normalises
  *
- * Every image equals the single-device render bit for bit (tests/test_gpu_api.py).
+ * Every image equals the single-device render bit for bit: tested with partitions sharing
+ * one GPU (device list with repeats: the same partition, normalisation and assembly code,
+ * rows moved by device copies instead of RCCL; tests/test_gpu_parity.py) and, on a node
+ * with >= 2 GPUs, over RCCL (skipped on one-GPU boxes).
  * The scene is uploaded to every device (a few MB).  Plain C ABI, as include/rtamd.h.
  */
 #ifndef RTAMD_MULTI_H
@@ -29,7 +32,8 @@ extern "C" {
 typedef struct rt_multi rt_multi;
 
 /* The builder's scene on `n_devices` HIP devices (devices[0] assembles the image) and one
- * RCCL communicator per device (ncclCommInitAll).  row_block <= 0 means 8. */
+ * RCCL communicator per device (ncclCommInitAll).  row_block <= 0 means 8.  A list that
+ * repeats a device makes partitions sharing that GPU (no communicator: device copies). */
 int rt_multi_create(const rt_builder* b, int n_devices, const int* devices, int row_block, rt_multi** out);
 /* The same from a flat scene descriptor (include/rtamd.h). */
 int rt_multi_create_desc(const rt_scene_desc* d, int n_devices, const int* devices, int row_block, rt_multi** out);

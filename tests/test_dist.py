@@ -144,3 +144,25 @@ def test_batched_row_gather(oracle, world, block):
         assert p.exitcode == 0
     for f in range(3):
         assert np.array_equal(got[f], want * (f + 1))
+
+
+@pytest.mark.parametrize("io", [False, True])
+def test_single_rank_frame_is_the_single_render(oracle, io):
+    """world 1 (no process group): the rank's selection is the whole image, which the
+    renderer already normalised for --intersection-only; render_frame must not divide by
+    the maximum a second time (dist.py)."""
+    from rtamd import dist as rd
+    import pyoracle
+    w, h, bdepth = 31, 19, 3
+    path = os.path.join(SCENES, "inputs/input-02.rti")
+    want, _ = oracle.render(path, w, h, bdepth=bdepth, intersection_only=io)
+
+    def render_rows(rows):
+        begin, end, step, block = rows
+        assert (begin, end, step) == (0, h, 1)
+        img, _ = pyoracle.render(path, w, h, bdepth=bdepth, intersection_only=io, threads=2)
+        # a renderer reports its raw maximum; here the image is normalised, so any value > 1
+        # would expose a second normalisation
+        return torch.from_numpy(img), 7.0
+    frame = rd.render_frame(render_rows, h, io, torch.device("cpu"), block=8)
+    assert np.array_equal(frame.numpy(), want)
