@@ -336,8 +336,10 @@ def roofline(solo, frames, traffic_path, concurrent, valu_path=None):
                 roofs["valu"] = {"achieved": vpl / t_launch_s / 1e9, "peak": vj["peak_wave_instr_per_s"] / 1e9,
                                  "unit": "G wave-instr/s",
                                  "what": "PMC SQ_INSTS_VALU per launch (wave64 vector instructions, " +
-                                         os.path.relpath(valu_path, REPO) + ") / solo launch time vs the sustained "
-                                         "v_fma_f32 issue rate of the whole chip (tools/valu_calibration.py)"}
+                                         os.path.relpath(valu_path, REPO) + ") / solo launch time vs " +
+                                         vj.get("peak_what", "the calibrated VALU issue rate"),
+                                 "counters": {k: vj[k].get(name) for k in ("valu_busy", "wait_any", "wait_inst_any")
+                                              if isinstance(vj.get(k), dict)}}
         except (OSError, ValueError):
             pass
     if traffic:

@@ -1705,10 +1705,12 @@ int rt_debug_fetch_calibration(int device, int64_t bytes) {
 	return RT_OK;
 }
 
-// Diagnostic (not in rtamd.h): VALU issue calibration.  k_valu_peak<float> and <double>
-// dispatches of `iters` rounds at 16 and 32 waves per CU (each after a warm-up); profiled with
-// rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace, instructions / duration is the sustained
-// wave64 VALU issue rate of fma chains (tools/valu_calibration.py).
+// Diagnostic (not in rtamd.h): VALU issue calibration.  k_valu_peak dispatches for each
+// instruction kind (v_fma_f32, v_pk_fma_f32, v_fma_f64) at 1, 2, 4 and 8 waves per SIMD
+// (each after a warm-up at the same shape), iterations scaled so that every dispatch issues
+// the same instructions per SIMD; profiled with rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU
+// SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE ..., they give cycles per wave64 instruction and the
+// shader clock (tools/valu_calibration.py, tools/make_valu.py).
 int rt_debug_valu_calibration(int device, int iters) {
 	HIP_TRY(hipSetDevice(device));
 	struct Sink {
@@ -1718,11 +1720,11 @@ int rt_debug_valu_calibration(int device, int iters) {
 		}
 	} sink;
 	HIP_TRY(hipMalloc(&sink.p, 64));
-	// fp32 and fp64 chains at 16 and 32 waves per CU (4 and 8 per SIMD)
-	for (int f64 = 0; f64 < 2; f64++)
-		for (int waves = 16; waves <= 32; waves *= 2) {
-			HIP_TRY(rtamd::launch_valu_peak(iters / 8 + 1, f64, waves, sink.p, nullptr));  // warm-up (clocks)
-			HIP_TRY(rtamd::launch_valu_peak(iters, f64, waves, sink.p, nullptr));
+	for (int kind = 0; kind < 3; kind++)
+		for (int w = 1; w <= 8; w *= 2) {
+			const int it = std::max(1, iters * 8 / w);
+			HIP_TRY(rtamd::launch_valu_peak(std::max(1, it / 8), kind, w, sink.p, nullptr));  // warm-up (clocks)
+			HIP_TRY(rtamd::launch_valu_peak(it, kind, w, sink.p, nullptr));
 		}
 	HIP_TRY(hipDeviceSynchronize());
 	return RT_OK;

@@ -169,7 +169,9 @@ hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uin
 constexpr int kPhaseSlots = 8;
 hipError_t read_phase_profile(unsigned long long* out /* 4 * kPhaseSlots */);
 // FETCH_SIZE calibration: reads `bytes` of buf once, `width` (1, 4, 8, 16) bytes per lane
-hipError_t launch_valu_peak(int iters, bool f64, int waves_per_cu, void* sink, hipStream_t stream);
+// VALU issue calibration: kind 0 v_fma_f32, 1 v_pk_fma_f32, 2 v_fma_f64 chains at
+// waves_per_simd waves on every SIMD
+hipError_t launch_valu_peak(int iters, int kind, int waves_per_simd, void* sink, hipStream_t stream);
 hipError_t launch_stream_read(const void* buf, int64_t bytes, int width, unsigned long long* sink, hipStream_t stream);
 hipError_t launch_selftest_math(int op, const double* x, const double* y, double* out, int64_t n, hipStream_t stream);
 

@@ -13,6 +13,7 @@
 // colour = (local + refraction) + reflection * kr (scene.cpp:127,134).
 // Device arithmetic: see intersect.h; pow is glibc's (glibc_pow.h).
 #include <algorithm>
+#include <type_traits>
 #include "trace.h"
 #include "glibc_pow.h"
 #include "intersect.h"
@@ -743,28 +744,44 @@ __global__ void k_stream_read(const T* __restrict__ p, int64_t n, unsigned long 
 }
 
 // VALU issue calibration (tools/valu_calibration.py, profiles/): every wave runs `iters`
-// rounds of 8 independent fma chains in T, 16 waves per CU on every CU, nothing else: the
-// chip's sustained rate of wave64 vector instructions of that kind (SQ_INSTS_VALU per
-// second), the peak of the roofline's VALU roof.
-template <typename T>
-__global__ void __launch_bounds__(256) k_valu_peak(int iters, T seed, T* sink) {
-	T a[8];
+// rounds of 32 independent chains, unrolled 4x (128 instructions per round, nothing else
+// in the loop but the counter), on every CU at W waves per SIMD (grid 256 W blocks of 4
+// waves).  K selects the instruction: 0 v_fma_f32, 1 v_pk_fma_f32 (two f32 FMAs per lane),
+// 2 v_fma_f64.  Operands are the chain's own register and inline constants (0.5, 1.0: the
+// chains converge to 2, never to a denormal or infinity), so no operand read limits issue.
+// rocprofv3 (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE + kernel trace) turns it
+// into cycles per wave64 instruction per SIMD and the shader clock.
+template <int K>
+__global__ void __launch_bounds__(256) k_valu_peak(int iters, float seed, float* sink) {
+	constexpr int kChains = 32;
+	using T = typename std::conditional<K == 2, double, float>::type;
+	constexpr int kLanes = K == 1 ? 2 : 1;  // v_pk_fma_f32 works on a pair of f32 registers
+	T a[kChains][kLanes];
 #pragma unroll
-	for (int k = 0; k < 8; k++) a[k] = seed + static_cast<T>(threadIdx.x + k);
-	const T m = static_cast<T>(0.999), c = static_cast<T>(1e-3);
+	for (int k = 0; k < kChains; k++)
+#pragma unroll
+		for (int l = 0; l < kLanes; l++) a[k][l] = static_cast<T>(seed + threadIdx.x + k + l);
 	for (int i = 0; i < iters; i++) {
 #pragma unroll
-		for (int k = 0; k < 8; k++) {
-			if constexpr (sizeof(T) == 4)  // one v_fma_f32 each (no v_pk_fma_f32 pairing)
-				asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(m), "v"(c));
-			else
-				a[k] = fma(a[k], m, c);
-		}
+		for (int u = 0; u < 4; u++)
+#pragma unroll
+			for (int k = 0; k < kChains; k++) {
+				if constexpr (K == 0) {
+					asm volatile("v_fma_f32 %0, %0, 0.5, 1.0" : "+v"(a[k][0]));
+				} else if constexpr (K == 1) {
+					asm volatile("v_pk_fma_f32 %0, %0, 0.5, 1.0 op_sel_hi:[1,0,0]"
+					             : "+v"(*reinterpret_cast<HIP_vector_base<float, 2>::Native_vec_*>(&a[k][0])));
+				} else {
+					asm volatile("v_fma_f64 %0, %0, 0.5, 1.0" : "+v"(a[k][0]));
+				}
+			}
 	}
 	T acc = 0;
 #pragma unroll
-	for (int k = 0; k < 8; k++) acc += a[k];
-	if (acc == static_cast<T>(-1)) sink[0] = acc;  // keeps the chains; never true
+	for (int k = 0; k < kChains; k++)
+#pragma unroll
+		for (int l = 0; l < kLanes; l++) acc += a[k][l];
+	if (acc == static_cast<T>(-1)) sink[0] = static_cast<float>(acc);  // keeps the chains; never true
 }
 
 // multi-GPU image assembly on the first device: one thread per byte of the image, each
@@ -894,12 +911,14 @@ hipError_t launch_stream_read(const void* buf, int64_t bytes, int width, unsigne
 	return hipGetLastError();
 }
 
-hipError_t launch_valu_peak(int iters, bool f64, int waves_per_cu, void* sink, hipStream_t stream) {
-	const unsigned grid = 256 * std::max(1, waves_per_cu / 4);  // blocks of 4 waves on every CU
-	if (f64)
-		hipLaunchKernelGGL(k_valu_peak<double>, dim3(grid), dim3(256), 0, stream, iters, 1.0, static_cast<double*>(sink));
-	else
-		hipLaunchKernelGGL(k_valu_peak<float>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, static_cast<float*>(sink));
+hipError_t launch_valu_peak(int iters, int kind, int waves_per_simd, void* sink, hipStream_t stream) {
+	const unsigned grid = 256 * std::max(1, waves_per_simd);  // blocks of 4 waves (one per SIMD) on every CU
+	float* out = static_cast<float*>(sink);
+	switch (kind) {
+		case 0: hipLaunchKernelGGL(k_valu_peak<0>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, out); break;
+		case 1: hipLaunchKernelGGL(k_valu_peak<1>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, out); break;
+		default: hipLaunchKernelGGL(k_valu_peak<2>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, out); break;
+	}
 	return hipGetLastError();
 }
 

@@ -20,5 +20,5 @@ for f in scene_host bvh png; do
 	g++ $FL -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c -o $B/$f.o $P/csrc/$f.cpp &
 done
 wait
-$HIPCC --offload-arch=gfx950 -shared -o $P/rtamd/var/librtamd_$TAG.so $B/trace.o $B/api.o $B/scene_host.o $B/bvh.o $B/png.o -lz
+$HIPCC --offload-arch=gfx950 -shared -o $P/rtamd/var/librtamd_$TAG.so $B/trace.o $B/api.o $B/scene_host.o $B/bvh.o $B/png.o -lz -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib
 echo "$P/rtamd/var/librtamd_$TAG.so"

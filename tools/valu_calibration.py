@@ -13,6 +13,6 @@ import rtamd  # noqa: E402
 L = rtamd.lib()
 L.rt_debug_valu_calibration.restype = ctypes.c_int
 L.rt_debug_valu_calibration.argtypes = [ctypes.c_int, ctypes.c_int]
-rc = L.rt_debug_valu_calibration(0, int(sys.argv[1]) if len(sys.argv) > 1 else 20000)
+rc = L.rt_debug_valu_calibration(0, int(sys.argv[1]) if len(sys.argv) > 1 else 2000)
 print({"rc": rc})
 sys.exit(0 if rc == 0 else 1)
