@@ -1076,9 +1076,17 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 		rt_scene_destroy(s.release());
 		return rc;
 	}
-	s->ds.cam = fs.camera;
+	{
+		std::vector<rtamd::DCamera> cam(1, fs.camera);
+		if ((rc = upload(s.get(), cam, &s->ds.cam))) {
+			rt_scene_destroy(s.release());
+			return rc;
+		}
+	}
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_may_raise = fs.n_may_raise;
+	s->ds.treelet_root = fs.treelet_root;
+	s->ds.treelet_count = std::min(fs.treelet_count, rtamd::kTreeletNodes);
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	// j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
 	std::vector<int32_t> shadow_light;

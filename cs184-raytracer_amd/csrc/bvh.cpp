@@ -184,6 +184,35 @@ struct Builder {
 	}
 };
 
+// Treelet layout: the top inner nodes of a mesh's LBVH renumbered into
+// breadth-first order right after its root, so that nodes [root, root + n) are the mesh's top
+// levels; the per-lane traversal reads those from a copy in LDS.  Only the node numbering
+// changes (child references follow it): boxes, leaves and every result are unchanged.
+int treelet_order(std::vector<DBvhNode>& nodes, size_t base, int max_nodes) {
+	const size_t n = nodes.size() - base;
+	if (n == 0) return 0;
+	std::vector<int32_t> bfs;  // local indices in breadth-first order (inner nodes only)
+	bfs.push_back(0);
+	for (size_t k = 0; k < bfs.size() && static_cast<int>(bfs.size()) < max_nodes; k++) {
+		const DBvhNode& nd = nodes[base + bfs[k]];
+		for (int c = 0; c < 2 && static_cast<int>(bfs.size()) < max_nodes; c++)
+			if (nd.count[c] == 0) bfs.push_back(nd.first[c] - static_cast<int32_t>(base));
+	}
+	std::vector<int32_t> to_new(n, -1);
+	int32_t next = 0;
+	for (int32_t v : bfs) to_new[v] = next++;
+	for (size_t v = 0; v < n; v++)
+		if (to_new[v] < 0) to_new[v] = next++;
+	std::vector<DBvhNode> old(nodes.begin() + base, nodes.end());
+	for (size_t v = 0; v < n; v++) {
+		DBvhNode nd = old[v];
+		for (int c = 0; c < 2; c++)
+			if (nd.count[c] == 0) nd.first[c] = static_cast<int32_t>(base) + to_new[nd.first[c] - static_cast<int32_t>(base)];
+		nodes[base + to_new[v]] = nd;
+	}
+	return static_cast<int>(bfs.size());
+}
+
 // Padded world-space box of an object-space box (the eight corners through fwd).  Used
 // only to skip geometries a ray cannot hit; a degenerate transform disables it.
 void world_box(const Geometry& g, const double lo[3], const double hi[3], DGeom& d) {
@@ -440,6 +469,13 @@ FlatScene flatten_scene(const Scene& s) {
 			break;
 		}
 		d.bvh_root = static_cast<int32_t>(node_base);
+		const int tl = treelet_order(fs.nodes, node_base, kTreeletNodes);
+		// the scene's treelet: the top levels of its largest LBVH mesh
+		if (g.face_count > fs.treelet_faces) {
+			fs.treelet_faces = g.face_count;
+			fs.treelet_root = d.bvh_root;
+			fs.treelet_count = tl;
+		}
 		fs.geoms.push_back(d);
 	}
 	// shadow-test order: spheres and linear meshes first, then BVH meshes by size

@@ -27,6 +27,12 @@ constexpr int kLeafFaces = RT_LEAF_FACES;  // faces per LBVH leaf
 #define RT_STACK_DEPTH 32
 #endif
 constexpr int kStackDepth = RT_STACK_DEPTH;  // traversal stack entries per lane (LDS); LBVH depth <= kStackDepth - 2
+// top inner nodes of the largest LBVH mesh copied into every per-lane traversal block's LDS
+// (4 levels: 960 B); 0 disables the treelet
+#ifndef RT_TREELET_NODES
+#define RT_TREELET_NODES 0
+#endif
+constexpr int kTreeletNodes = RT_TREELET_NODES;
 
 struct alignas(16) DGeom {
 	double fwd[3][4];     // forwardTransform rows

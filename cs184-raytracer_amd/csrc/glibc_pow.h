@@ -29,11 +29,42 @@ RT_HD uint32_t top12(double x) { return static_cast<uint32_t>(bits(x) >> 52); }
 constexpr uint64_t kOff = 0x3fe6955500000000ULL;
 constexpr uint32_t kSignBias = 0x800 << 7;
 
+// The polynomial and reduction constants.  On the device they are read from constant memory
+// through a pointer the compiler cannot see through (scalar loads where pow runs): as
+// literals, a kernel that calls pow inside its grid-stride loop (the fused Phong terms of
+// k_shadow) materialises all of them in vector registers before the loop and spills them.
+struct PowConsts {
+	double ln2hi, ln2lo, logpoly[7];
+	double invln2n, shift, negln2hin, negln2lon, exppoly[4];
+};
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__ PowConsts kPowConstsDev = {
+    glibc_pow_data::kLn2hi, glibc_pow_data::kLn2lo,
+    {glibc_pow_data::kLogPoly[0], glibc_pow_data::kLogPoly[1], glibc_pow_data::kLogPoly[2], glibc_pow_data::kLogPoly[3],
+     glibc_pow_data::kLogPoly[4], glibc_pow_data::kLogPoly[5], glibc_pow_data::kLogPoly[6]},
+    glibc_pow_data::kInvLn2N, glibc_pow_data::kShift, glibc_pow_data::kNegLn2hiN, glibc_pow_data::kNegLn2loN,
+    {glibc_pow_data::kExpPoly[0], glibc_pow_data::kExpPoly[1], glibc_pow_data::kExpPoly[2], glibc_pow_data::kExpPoly[3]}};
+__device__ __forceinline__ const __attribute__((address_space(4))) PowConsts& pow_consts() {
+	const PowConsts* p = &kPowConstsDev;
+	asm volatile("" : "+s"(p));
+	return *(const __attribute__((address_space(4))) PowConsts*)(p);
+}
+#define RT_POW_CONSTS const auto& C = pow_consts()
+#else
+constexpr PowConsts kPowConstsHost = {
+    glibc_pow_data::kLn2hi, glibc_pow_data::kLn2lo,
+    {glibc_pow_data::kLogPoly[0], glibc_pow_data::kLogPoly[1], glibc_pow_data::kLogPoly[2], glibc_pow_data::kLogPoly[3],
+     glibc_pow_data::kLogPoly[4], glibc_pow_data::kLogPoly[5], glibc_pow_data::kLogPoly[6]},
+    glibc_pow_data::kInvLn2N, glibc_pow_data::kShift, glibc_pow_data::kNegLn2hiN, glibc_pow_data::kNegLn2loN,
+    {glibc_pow_data::kExpPoly[0], glibc_pow_data::kExpPoly[1], glibc_pow_data::kExpPoly[2], glibc_pow_data::kExpPoly[3]}};
+#define RT_POW_CONSTS const PowConsts& C = kPowConstsHost
+#endif
+
 // log(x) = hi + lo for the (normalised) bit pattern ix; kLogTab may live in LDS
 RT_HD double log_inline(uint64_t ix, double* tail, const double* kLogTab) {
-	using glibc_pow_data::kLn2hi;
-	using glibc_pow_data::kLn2lo;
-	using glibc_pow_data::kLogPoly;
+	RT_POW_CONSTS;
+	const double kLn2hi = C.ln2hi, kLn2lo = C.ln2lo;
+	const auto& kLogPoly = C.logpoly;
 	const uint64_t tmp = ix - kOff;
 	const int i = static_cast<int>((tmp >> 45) % 128);
 	const int k = static_cast<int>(static_cast<int64_t>(tmp) >> 52);
@@ -88,11 +119,9 @@ RT_HD double specialcase(double tmp, uint64_t sbits, uint64_t ki) {
 }
 
 RT_HD double exp_inline(double x, double xtail, uint32_t sign_bias, const uint64_t* kExpTab) {
-	using glibc_pow_data::kExpPoly;
-	using glibc_pow_data::kInvLn2N;
-	using glibc_pow_data::kNegLn2hiN;
-	using glibc_pow_data::kNegLn2loN;
-	using glibc_pow_data::kShift;
+	RT_POW_CONSTS;
+	const double kInvLn2N = C.invln2n, kShift = C.shift, kNegLn2hiN = C.negln2hin, kNegLn2loN = C.negln2lon;
+	const auto& kExpPoly = C.exppoly;
 	uint32_t abstop = top12(x) & 0x7ff;
 	if (abstop - 0x3c9 >= 0x408 - 0x3c9) {  // |x| < 2^-54 or |x| >= 512
 		if (static_cast<int32_t>(abstop - 0x3c9) < 0) {

@@ -54,6 +54,14 @@ template <typename T>
 __device__ __forceinline__ const __attribute__((address_space(4))) T* uniform_ptr(const T* p) {
 	return (const __attribute__((address_space(4))) T*)(p);
 }
+// A pointer the compiler cannot see through at this point of the program: loads through it
+// cannot be hoisted above here (e.g. out of a kernel's grid-stride loop, where the loaded
+// values would occupy scalar registers for the whole kernel and spill).
+template <typename T>
+__device__ __forceinline__ const T* opaque(const T* p) {
+	asm volatile("" : "+s"(p));
+	return p;
+}
 template <bool kUniform, typename T>
 __device__ __forceinline__ auto scene_ptr(const T* p) {
 	if constexpr (kUniform)
@@ -79,7 +87,64 @@ __device__ __forceinline__ double dot4z(V3 a, V3 b) { return (a.x * b.x + a.z * 
 __device__ __forceinline__ double sq4(V3 a) { return (a.x * a.x + a.z * a.z) + a.y * a.y; }
 // isZero(): all |c| <= 1e-12 (w is zero)
 __device__ __forceinline__ bool is_zero3(V3 a) { return fabs(a.x) <= 1e-12 && fabs(a.y) <= 1e-12 && fabs(a.z) <= 1e-12; }
+// Exact binary64 division with a shared divisor (RT_SHARED_DIV).  The compiler expands
+// every `a / b` into v_div_scale x2, v_rcp_f64, two Newton steps, a product, a residual,
+// v_div_fmas and v_div_fixup (11 instructions), and recomputes the reciprocal for each
+// quotient because v_div_scale depends on the numerator.  When neither operand needs
+// v_div_scale's scaling and the quotient is normal (|a|, |b| in [2^-300, 2^300]: exponent
+// gap < 768, no denormal 1/b or a/b, numerator exponent > 53) v_div_scale returns its operand
+// unchanged with VCC clear, v_div_fmas is a plain fma and v_div_fixup returns its input, so
+//   r = rcp(b); r = fma(r, fma(-b, r, 1), r) twice; q0 = a * r; q = fma(fma(-b, q0, a), r, q0)
+// is the hardware sequence itself, bit for bit, with r computed once per divisor (3
+// instructions per further quotient).  Any other operand takes the compiler's division.
+#ifndef RT_SHARED_DIV
+#define RT_SHARED_DIV 0
+#endif
+struct Recip {
+	double b, r;
+	bool ok;  // b in the range above
+};
+__device__ __forceinline__ bool div_range(double x) {
+	const double f = fabs(x);
+	return f >= 0x1p-300 && f <= 0x1p300;
+}
+__device__ __forceinline__ Recip recip(double b) {
+	Recip R;
+	R.b = b;
+	R.ok = RT_SHARED_DIV && div_range(b);
+	double r = __builtin_amdgcn_rcp(b);
+	r = fma(r, fma(-b, r, 1.0), r);
+	r = fma(r, fma(-b, r, 1.0), r);
+	R.r = r;
+	return R;
+}
+__device__ __forceinline__ double qdiv(double a, const Recip& R) {
+	if (__builtin_expect(R.ok && div_range(a), 1)) {
+		const double q0 = a * R.r;
+		return fma(fma(-R.b, q0, a), R.r, q0);
+	}
+	return a / R.b;
+}
 __device__ __forceinline__ V3 div3(V3 a, double n) { return mk(a.x / n, a.y / n, a.z / n); }
+// a.normalized() = a / |a| (Eigen divides by the norm): sqrt of ((x^2 + z^2) + y^2), then
+// three quotients sharing the divisor.  One decision for all three: the norm's square in
+// [2^-600, 2^600] puts the divisor in range, and a nonzero square of every component puts it
+// above 2^-538 (so |a_i / n| >= 2^-838; |a_i| <= n bounds it above); a zero component (its
+// sign of zero) or any other case takes the compiler's divisions.
+__device__ __forceinline__ V3 normalized3(V3 a, double* norm = nullptr) {
+	const double xx = a.x * a.x, yy = a.y * a.y, zz = a.z * a.z;
+	const double n2 = (xx + zz) + yy;  // sq4 (w == 0)
+	const double n = sqrt(n2);
+	if (norm) *norm = n;
+	if (RT_SHARED_DIV && n2 >= 0x1p-600 && n2 <= 0x1p600 && xx != 0 && yy != 0 && zz != 0) {
+		double r = __builtin_amdgcn_rcp(n);
+		r = fma(r, fma(-n, r, 1.0), r);
+		r = fma(r, fma(-n, r, 1.0), r);
+		const double qx = a.x * r, qy = a.y * r, qz = a.z * r;
+		return mk(fma(fma(-n, qx, a.x), r, qx), fma(fma(-n, qy, a.y), r, qy), fma(fma(-n, qz, a.z), r, qz));
+	}
+	return div3(a, n);
+}
 
 template <typename M>
 __device__ __forceinline__ V3 xf_point(M m, V3 p) {
@@ -104,7 +169,7 @@ __device__ __forceinline__ void raise_error(DeviceCounters* c, int code) { atomi
 // Ray::direction(dir) (rtbase.h:17-23): reject |c| <= 1e-12, then dir.normalized()
 __device__ __forceinline__ V3 ray_dir(V3 d, DeviceCounters* c) {
 	if (is_zero3(d)) raise_error(c, DERR_NO_DIRECTION);
-	return div3(d, sqrt(sq4(d)));
+	return normalized3(d);
 }
 
 // Matrix3d::determinant of the matrix with columns c0, c1, c2 (LU/Determinant.h:61-69)
@@ -309,17 +374,18 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	if (D == 0) return false;
 	const double Da = det3(rhs, vb, nd);
 	if (quotient_surely_negative(Da, D) || quotient_surely_above(Da, D, 1.0)) return false;
-	const double a = Da / D;
+	const Recip RD = recip(D);  // Cramer's three quotients share the divisor
+	const double a = qdiv(Da, RD);
 	if (a < 0 || a > 1) return false;
 	const double Db = det3(va, rhs, nd);
 	if (quotient_surely_negative(Db, D) || quotient_surely_above(Db, D, 1.0)) return false;
-	const double b = Db / D;
+	const double b = qdiv(Db, RD);
 	if (b < 0 || a + b > 1) return false;
 	const double Dt = det3(va, vb, rhs);
 	if (quotient_surely_negative(Dt, D)) return false;
 	// dist = t * dn with dn = |d|_3 within a few ulps of 1: t > 1.001 * best * 1.001 cannot win
 	if (best.dist < INFINITY && best.dist >= 0x1p-900 && quotient_surely_above(Dt, D, best.dist * 1.001)) return false;
-	const double t = Dt / D;
+	const double t = qdiv(Dt, RD);
 	if (t < 0) return false;
 	const double dist = t * dn;
 	if (!(dist < best.dist || (dist == best.dist && id < best.id))) return false;
@@ -424,6 +490,46 @@ __device__ __forceinline__ bool slab32(P lo, P hi, const Ray32& r, float lim, fl
 
 
 
+// The treelet (bvh.cpp treelet_order): the top inner nodes of the scene's largest LBVH mesh,
+// copied into LDS by every per-lane traversal block (load_treelet) and read from there by
+// mesh_search: the first levels of every descent cost an LDS read instead of a dependent L2
+// round trip.  (Module-scope LDS: allocated only in the kernels that reach mesh_search.)
+__shared__ DBvhNode g_treelet[kTreeletNodes > 0 ? kTreeletNodes : 1];
+
+__device__ __forceinline__ void load_treelet(const DeviceScene& S) {
+	if (kTreeletNodes > 0) {
+		constexpr int kPieces = sizeof(DBvhNode) / sizeof(uint4);
+		const int n = S.treelet_count * kPieces;
+		const uint4* src = reinterpret_cast<const uint4*>(S.nodes + (S.treelet_root < 0 ? 0 : S.treelet_root));
+		uint4* dst = reinterpret_cast<uint4*>(g_treelet);
+		for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
+	}
+	__syncthreads();
+}
+
+// A node record in registers: the child boxes and the child references
+struct NodeRec {
+	float lo[2][3], hi[2][3];
+	int4 refs;  // first[0], first[1], count[0], count[1]
+};
+__device__ __forceinline__ void read_node(const DBvhNode* N, NodeRec& r) {
+#pragma unroll
+	for (int c = 0; c < 2; c++)
+#pragma unroll
+		for (int a = 0; a < 3; a++) {
+			r.lo[c][a] = N->lo[c][a];
+			r.hi[c][a] = N->hi[c][a];
+		}
+	r.refs = *reinterpret_cast<const int4*>(N->first);
+}
+__device__ __forceinline__ void fetch_node(const DeviceScene& S, int32_t ref, NodeRec& r) {
+	const uint32_t tli = static_cast<uint32_t>(ref - S.treelet_root);
+	if (kTreeletNodes > 0 && tli < static_cast<uint32_t>(S.treelet_count))
+		read_node(g_treelet + tli, r);
+	else
+		read_node(S.nodes + ref, r);
+}
+
 // Mesh::calculateIntNormInObjSpace (geometry.cpp:69-126) with an LBVH in place of the
 // linear scan for large meshes.
 //   kAnyHit = false: the reference's closest face (returns found, Po, No).
@@ -477,12 +583,13 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 			PROF_BEGIN(tn);
 			while (ref >= 0) {
 				ws.inc<W_NODES>();
-				const DBvhNode* N = S.nodes + ref;
 				// the child references are read with the boxes (one memory round trip per node)
-				const int4 refs = *reinterpret_cast<const int4*>(N->first);  // first[0], first[1], count[0], count[1]
+				NodeRec nr;
+				fetch_node(S, ref, nr);
+				const int4 refs = nr.refs;
 				float tn0, tn1;
-				const bool h0 = slab32(N->lo[0], N->hi[0], r32, lim, tn0);
-				const bool h1 = slab32(N->lo[1], N->hi[1], r32, lim, tn1);
+				const bool h0 = slab32(nr.lo[0], nr.hi[0], r32, lim, tn0);
+				const bool h1 = slab32(nr.lo[1], nr.hi[1], r32, lim, tn1);
 				if (h0 || h1) {
 					const int c = (h0 && h1) ? (tn1 < tn0 ? 1 : 0) : (h1 ? 1 : 0);
 					const int32_t cf = c ? refs.y : refs.x, cc = c ? refs.w : refs.z;
@@ -592,7 +699,7 @@ __device__ __forceinline__ void winner_point_normal(const DeviceScene& S, int g,
 	if (h.face < 0) {
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
-		Po = oo + h.a * div3(draw, sqrt(sq4(draw)));
+		Po = oo + h.a * normalized3(draw);
 		No = Po - load3(G->center);
 	} else {
 		Po = face_point(S, h);
@@ -674,8 +781,8 @@ __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool rever
 	const V3 oo = xf_point(G->inv, o);
 	const V3 draw = xf_dir(G->inv, d);
 	if (is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
-	const double nrm = sqrt(sq4(draw));  // object-space length of the unit world direction
-	const V3 dd = div3(draw, nrm);
+	double nrm;  // object-space length of the unit world direction
+	const V3 dd = normalized3(draw, &nrm);
 	PROF_END(ws, PH_XFORM, tx);
 	FaceHit h{-1, 0, 0};
 	bool hit, settled = false;
@@ -879,7 +986,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
-		const V3 dd = div3(draw, sqrt(sq4(draw)));
+		const V3 dd = normalized3(draw);
 		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
 		bool hit, settled;
@@ -930,8 +1037,8 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
-		const double nrm = sqrt(sq4(draw));
-		const V3 dd = div3(draw, nrm);
+		double nrm;
+		const V3 dd = normalized3(draw, &nrm);
 		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
 		bool hit, settled = false;

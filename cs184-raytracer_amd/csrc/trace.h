@@ -18,10 +18,13 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DFaceNrm* fnrm;
 	const DBvhNode* nodes;
 	const int32_t* shadow_order;              // geometry order of the occlusion query
-	DCamera cam;
+	// the camera (device copy): read where primary rays are made, not held in registers for
+	// the kernel's lifetime as a 160-B by-value kernel argument would be
+	const DCamera* cam;
 	int32_t n_geoms, n_lights, n_nonambient;
 	int32_t n_may_raise;                      // geometries with DGeom::may_raise
 	const int32_t* shadow_light;              // j-th non-ambient light -> light index
+	int32_t treelet_root, treelet_count;      // nodes [root, root + count) staged in LDS (per-lane traversal)
 };
 
 // One wavefront level of ray records (structure of arrays).

@@ -50,8 +50,9 @@ constexpr int kShadeBlock = 512;
 #endif
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
-__device__ __forceinline__ void primary_ray(const DCamera& cam, int r, int c, int W, int H, V3& o, V3& d,
+__device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, int W, int H, V3& o, V3& d,
                                             DeviceCounters* ctr) {
+	const auto& cam = *uniform_ptr(opaque(camp));
 	const double rF = (r + 0.5) / H;
 	const double cF = (c + 0.5) / W;
 	const double rI = 1.0 - rF, cI = 1.0 - cF;
@@ -69,7 +70,7 @@ __device__ __forceinline__ void primary_ray(const DCamera& cam, int r, int c, in
 	else if (dw != 0)
 		raise_error(ctr, DERR_POINT_DIRECTION);
 	o = load3(cam.eye);
-	d = div3(dv, sqrt(sq4(dv)));
+	d = normalized3(dv);
 }
 
 template <typename LV>
@@ -197,11 +198,14 @@ __device__ __forceinline__ Slots block_append2(bool a, bool b0, bool b1, int32_t
 // shading, so they are spawned here and level L+1 can be traced while level L is shaded.
 // One item (thread t of the level's index space) of k_closest; every thread of the block
 // calls it (block_append2 synchronises the block).
-template <bool kPacket, typename LV>
+template <bool kPacket>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
-                                             int remaining, int plan_last, const LV& cur, const LV& next,
+                                             int remaining, int plan_last, const RayLevel* levels,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
                                              AppendLds& append_lds, int32_t* stack, uint32_t* stat_lds) {
+	// the level records (~30 buffer pointers) are read where they are used, before and after
+	// the traversal, not held in scalar registers through it
+	const int next_level = remaining > 0 ? level + 1 : level;
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
 	WorkStats ws{};
@@ -214,7 +218,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	bool inside = false;
 	V3 o = mk(0, 0, 0), d = mk(0, 0, 1);
 	PROF_BEGIN(t_setup);
-	if (active) level_ray(S, fg, level, i, cur, o, d, inside, ctr);
+	if (active) level_ray(S, fg, level, i, *uniform_ptr(opaque(levels) + level), o, d, inside, ctr);
 	PROF_END(ws, PH_SETUP, t_setup);
 #if RT_DIAG_LANES
 	if (!kPacket) diag_lanes(0, active);  // [0] wave slots, [1] active lanes of k_closest<false>
@@ -262,6 +266,9 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 			spawn_refl = true;
 		}
 	}
+	const RayLevel* lv = opaque(levels);
+	const auto& cur = *uniform_ptr(lv + level);
+	const auto& next = *uniform_ptr(lv + next_level);
 	const Slots slot = block_append2(shade, spawn_refr, spawn_refl, cur.counts, cur.counts + 1, append_lds);
 	{
 		const unsigned long long m_hit = __ballot(shade), m_refl = __ballot(spawn_refl), m_refr = __ballot(spawn_refr);
@@ -348,22 +355,24 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	if constexpr (!kPacket) load_treelet(S);
 	// level records read through the constant address space (scalar loads at their uses)
-	const auto& cur = *uniform_ptr(levels + level);
-	const auto& next = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
+	const auto& cur0 = *uniform_ptr(levels + level);
+	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
 	// the level's rays: n_host, or the previous level's child counter, never more than the
 	// level holds (children beyond its capacity were not written, see closest_item)
-	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur.capacity) : n_host;
+	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur0.capacity) : n_host;
 	if (blockIdx.x == 0 && threadIdx.x == 0) {
 		// the next level's counts start at zero (its k_closest appends to them)
-		if (remaining > 0) next.counts[0] = next.counts[1] = 0;
+		if (remaining > 0) next0.counts[0] = next0.counts[1] = 0;
 		if (n) atomicAdd(stats + ST_RAYS, static_cast<unsigned long long>(n));  // traceRay calls
 	}
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride)
-		closest_item<kPacket>(S, fg, level, n, remaining, plan_last, cur, next, ctr, stats, base + threadIdx.x,
+	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
+		closest_item<kPacket>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
 		                      append_lds, stack, stat_lds);
+	}
 }
 
 // Level of item t of a batch (wave-uniform: every level's items start on a wave boundary,
@@ -465,15 +474,41 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 //    towards each light in turn (one light at a time, still wave-uniform), loading the hit
 //    records once for all lights.
 // The light record of the wave is read with scalar loads.
+// Hit records of the packet shadow kernel staged in LDS (RT_HIT_LDS): the hit point and
+// normal (and the viewing direction of the fused shading) are read from the block's LDS for
+// every light and for the Phong terms instead of occupying 18 VGPRs through every traversal.
+#ifndef RT_HIT_LDS
+#define RT_HIT_LDS 0
+#endif
+typedef __attribute__((address_space(3))) double lds_f64;
+// an LDS address the compiler cannot see through: the values are read back from LDS, not
+// kept in registers from the store (which is what staging them avoids)
+__device__ __forceinline__ lds_f64* opaque_lds(lds_f64* p) {
+	asm volatile("" : "+v"(p));
+	return p;
+}
+struct HitStage {
+	lds_f64* p;  // this lane's slots: p[k * kBlock], k = 0..8 (P, N, d)
+	__device__ __forceinline__ void put(int k, V3 v) {
+		p[(3 * k + 0) * kBlock] = v.x;
+		p[(3 * k + 1) * kBlock] = v.y;
+		p[(3 * k + 2) * kBlock] = v.z;
+	}
+	__device__ __forceinline__ V3 get(int k) const {
+		const lds_f64* q = opaque_lds(p);
+		return mk(q[(3 * k + 0) * kBlock], q[(3 * k + 1) * kBlock], q[(3 * k + 2) * kBlock]);
+	}
+};
+
 template <bool kPacket>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
-                                            uint32_t* stat_lds) {
+                                            uint32_t* stat_lds, double* hit_lds) {
+	constexpr bool kStage = kPacket && RT_HIT_LDS;
 	const int nl = S.n_nonambient;
 	const BatchItem it = batch_item<true>(B, nl, tg);
 	const int level = it.level;
 	const int64_t t = it.local, nh = it.nh;
-	const auto& cur = *uniform_ptr(levels + level);
 	WorkStats ws{};
 	ws.init(stat_lds);
 	PROF_BEGIN(t_total);
@@ -492,18 +527,35 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	const bool on = h < nh;
 	V3 P = mk(0, 0, 0), N = mk(0, 0, 1);
 	bool inside = false, zero_mat = false;
-	if (on) {
-		P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
-		N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
-		const uint8_t fl = cur.hinside[h];
-		inside = fl & 1;
-		zero_mat = fl & 2;
+	HitStage hs{(lds_f64*)(hit_lds) + threadIdx.x};
+	{
+		// the level's record, read here and again where the verdicts are written (opaque: its
+		// buffer pointers are not held in scalar registers through the traversals)
+		const auto& cur = *uniform_ptr(opaque(levels) + level);
+		if (on) {
+			P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
+			N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
+			const uint8_t fl = cur.hinside[h];
+			inside = fl & 1;
+			zero_mat = fl & 2;
+			if constexpr (kStage) {
+				hs.put(0, P);
+				hs.put(1, N);
+				hs.put(2, mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]));
+			}
+		}
 	}
 	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
 	for (int j = j0; j < j1; j++) {
 		V3 Ld = mk(0, 0, 1);
 		bool rev = false, zero = false;
 		double dL = 0;
+		if constexpr (kStage) {
+			if (on) {
+				P = hs.get(0);
+				N = hs.get(1);
+			}
+		}
 		if (on) {
 			const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
 			const bool point = L.kind == DLIGHT_POINT;
@@ -518,7 +570,14 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 			// the light is occluded or not (it is never -0), so the ray is not traced.
 			if (zero_mat && L.zero_terms && nl_dot <= 0.0) {
 				const V3 R = (2 * nl_dot) * N - Ld;
-				zero = -dot4z(mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]), R) <= 0.0;
+				V3 dv;
+				if constexpr (kStage) {
+					dv = hs.get(2);
+				} else {
+					const auto& cur = *uniform_ptr(opaque(levels) + level);
+					dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
+				}
+				zero = -dot4z(dv, R) <= 0.0;
 			}
 			// the reference's castRay still maps the ray into every object space (may raise)
 			if (zero) check_may_raise(S, Ld, true, ctr);
@@ -537,10 +596,12 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 		else if (trace)
 			occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
 		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
-		if (B.fused)
+		if (B.fused) {
 			verdicts |= static_cast<unsigned long long>(occ || zero) << j;
-		else if (on)
+		} else if (on) {
+			const auto& cur = *uniform_ptr(opaque(levels) + level);
 			cur.occl[j * cur.capacity + h] = occ || zero;
+		}
 		const unsigned long long mz = __ballot(zero);
 		if (mz && __lane_id() == 0) atomicAdd(shard(stats) + ST_SHADOW_ZERO, (unsigned long long)__popcll(mz));
 	}
@@ -548,10 +609,19 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	flush_stats(ws, stats, 1, kPacket);
 	// fused shading (ShadeBatch::fused: all lights of the hit traced by this lane): the Phong
 	// terms of k_shade from the verdicts in registers
-	if (kPacket && B.fused && on)
-		shade_hit(S, cur, h, P, N, mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]),
-		          [&](int j) { return static_cast<bool>((verdicts >> j) & 1); }, glibc_pow_data::kLogTab,
-		          glibc_pow_data::kExpTab, ctr);
+	if (kPacket && B.fused && on) {
+		const auto& cur = *uniform_ptr(opaque(levels) + level);
+		V3 dv;
+		if constexpr (kStage) {
+			P = hs.get(0);
+			N = hs.get(1);
+			dv = hs.get(2);
+		} else {
+			dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
+		}
+		shade_hit(S, cur, h, P, N, dv, [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
+		          glibc_pow_data::kLogTab, glibc_pow_data::kExpTab, ctr);
+	}
 }
 
 // Host-counted batches launch one thread per item; device-counted ones a fixed grid that
@@ -563,11 +633,13 @@ __global__ void __launch_bounds__(kBlock)
                                                                      unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
+	__shared__ double hit_lds[(kPacket && RT_HIT_LDS) ? 9 * kBlock : 1];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	if constexpr (!kPacket) load_treelet(S);
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
-		shadow_item<kPacket>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
+		shadow_item<kPacket>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds, hit_lds);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -720,12 +792,21 @@ __global__ void k_normalize(int64_t n_values, double* rgb, double rcp, uint8_t* 
 __global__ void k_selftest(int op, const double* x, const double* y, double* out, int64_t n) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	if (i >= n) return;
-	if (op == 0)
+	if (op == 0) {
 		out[i] = glibc_pow(x[i], y[i]);
-	else if (op == 1)
+	} else if (op == 1) {
 		out[i] = sqrt(x[i]);
-	else
+	} else if (op == 2) {
 		out[i] = x[i] / y[i];
+	} else if (op == 3) {  // the shared-divisor quotient of test_face (intersect.h qdiv)
+		out[i] = qdiv(x[i], recip(y[i]));
+	} else if (op == 4) {  // normalized3 of the vector (x[i], y[i], x[i + n]) (component x; .y, .z below)
+		out[i] = normalized3(mk(x[i], y[i], x[(i + n / 2) % n])).x;
+	} else if (op == 5) {
+		out[i] = normalized3(mk(x[i], y[i], x[(i + n / 2) % n])).y;
+	} else {
+		out[i] = normalized3(mk(x[i], y[i], x[(i + n / 2) % n])).z;
+	}
 }
 
 // FETCH_SIZE calibration (profiles/, MI355X_MICROARCH.md: the counter is calibrated only
