@@ -196,10 +196,10 @@ struct rt_scene {
 	int fail_after = -1;                         // fault injection (rt_debug_fail_after): launches left
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
 	// RTAMD_DIRECT_LEVELS: levels shaded beside the closest-hit chain; the rest are shaded in
-	// batches after it.  Measured best on C3: 2 for one frame per call
+	// batches after it.  Measured best on C3: 3 for one frame per call
 	// (latency: level 1's shading overlaps levels 2+), 1 for batches (throughput: fewer,
 	// larger shading launches while other frames fill the GPU).  The variable sets both.
-	int direct_levels_single = 2;
+	int direct_levels_single = 3;
 	int direct_levels_batch = 1;
 	int single_lanes = 1;                        // lanes one frame is split over (RTAMD_LANES)
 	int batch_lanes = 3;                         // frames of a batch in flight (RTAMD_BATCH_LANES)
@@ -220,6 +220,16 @@ struct rt_scene {
 	int plan_share = 1;                          // RTAMD_PLAN_SHARE
 	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
 	int shadow_all_lights = 3;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
+	// RTAMD_LIGHT_MAJOR_BELOW: a shading launch with fewer hits than this traces light-major
+	// (one lane per (hit, light)) even where the all-lights layout is selected: a few waves per
+	// SIMD each tracing every light in turn leave the GPU latency-bound (one GPU's row share
+	// of a single frame); light-major gives n_lights times the waves, each a shorter chain
+	int64_t light_major_below = 131072;
+	int all_lights_for(int first_level, int64_t hits) const {
+		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
+		if (al && ds.n_nonambient > 1 && hits < light_major_below) al = 0;
+		return al;
+	}
 	// RTAMD_DEEP_SPLIT: the first n levels after the direct ones are shaded alone, each in
 	// its own launch after the chain, before one batch of the rest (a batch's first bounce
 	// then traces its shadow rays as packets; per call like direct_levels)
@@ -415,7 +425,9 @@ struct Render {
 		auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
 		int64_t so = 0, ho = 0;
 		b.n = static_cast<int32_t>(lv.size());
-		b.all_lights = (s->shadow_all_lights >> (lv.front().first == 0 ? 0 : 1)) & 1;
+		int64_t hits = 0;
+		for (const auto& l : lv) hits += l.second;
+		b.all_lights = s->all_lights_for(lv.front().first, hits);
 		for (int k = 0; k < b.n; k++) {
 			b.level[k] = lv[k].first;
 			b.nh[k] = lv[k].second;
@@ -474,7 +486,9 @@ struct Render {
 		int64_t so = 0, ho = 0;  // upper bounds (the levels' capacities): grid sizes only
 		b.n = static_cast<int32_t>(lv.size());
 		b.dev_counts = 1;
-		b.all_lights = (s->shadow_all_lights >> (lv.front() == 0 ? 0 : 1)) & 1;
+		int64_t hits = 0;
+		for (int L : lv) hits += pl.hits[L];
+		b.all_lights = s->all_lights_for(lv.front(), hits);
 		for (int k = 0; k < b.n; k++) {
 			const rtamd::RayLevel& L = ln.levels[lv[k]].lv;
 			b.level[k] = lv[k];
@@ -1057,6 +1071,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
+	if (const char* lm = std::getenv("RTAMD_LIGHT_MAJOR_BELOW")) s->light_major_below = std::atoll(lm);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
 	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);

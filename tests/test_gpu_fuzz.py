@@ -100,7 +100,9 @@ _W, _H = (int(v) for v in os.environ.get("RTAMD_FUZZ_SIZE", "56x40").split("x"))
 
 
 @pytest.mark.parametrize("seed", range(_BASE, _BASE + _SEEDS))
-def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed):
+def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
+    # odd seeds: the production light-major threshold (every launch here is below it)
+    monkeypatch.setenv("RTAMD_LIGHT_MAJOR_BELOW", "131072" if seed % 2 else "0")
     path, bdepth, io = random_scene(seed, tmp_path)
     w, h = _W, _H
     try:

@@ -1,6 +1,7 @@
 """Renders one BASELINE.json config `reps` times into HBM (for rocprofv3 timelines).
 
-usage: python tools/one_config.py <config> [reps]"""
+usage: python tools/one_config.py <config> [reps] [k/n]   (k/n: rank k's 8-row-block share of an
+n-way partition, as bench.py's strong-scaling sweep renders it)"""
 import os
 import sys
 import time
@@ -19,6 +20,9 @@ s = rtamd.load_scene(os.path.join(SCENES, scene))
 out = torch.empty((h, w, 3), dtype=torch.float64, device="cuda")
 out8 = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
 prm = s.params(w, h, kw["bdepth"], kw["intersection_only"], 0, h, 1)
+if len(sys.argv) > 3:
+    k, n = (int(v) for v in sys.argv[3].split("/"))
+    prm = s.params(w, h, kw["bdepth"], kw["intersection_only"], k * 8, h, n, row_block=8)
 ts = []
 for _ in range(reps):
     torch.cuda.synchronize()
