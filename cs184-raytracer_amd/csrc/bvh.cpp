@@ -215,7 +215,24 @@ int treelet_order(std::vector<DBvhNode>& nodes, size_t base, int max_nodes) {
 
 // Padded world-space box of an object-space box (the eight corners through fwd).  Used
 // only to skip geometries a ray cannot hit; a degenerate transform disables it.
+// The fp32 world box of the device's world cull (intersect.h world_slab32): the padded box
+// widened by 2^-20 of its largest coordinate, rounded outward (infinite bounds stay infinite).
+void world_box32(DGeom& d, double amax) {
+	const double pad = 0x1p-20 * amax;
+	for (int k = 0; k < 3; k++) {
+		d.wlo32[k] = std::isfinite(d.wlo[k]) ? round_down_f32(d.wlo[k] - pad) : static_cast<float>(d.wlo[k]);
+		d.whi32[k] = std::isfinite(d.whi[k]) ? round_up_f32(d.whi[k] + pad) : static_cast<float>(d.whi[k]);
+	}
+}
+
+void world_box_impl(const Geometry& g, const double lo[3], const double hi[3], DGeom& d, double& amax);
 void world_box(const Geometry& g, const double lo[3], const double hi[3], DGeom& d) {
+	double amax = 0;
+	world_box_impl(g, lo, hi, d, amax);
+	world_box32(d, amax);
+}
+
+void world_box_impl(const Geometry& g, const double lo[3], const double hi[3], DGeom& d, double& amax) {
 	bool finite = std::isfinite(g.det) && g.det != 0;
 	for (int i = 0; i < 3; i++)
 		for (int j = 0; j < 4; j++) finite = finite && std::isfinite(g.fwd.m[i][j]) && std::isfinite(g.inv.m[i][j]);
@@ -232,7 +249,7 @@ void world_box(const Geometry& g, const double lo[3], const double hi[3], DGeom&
 		return;
 	}
 	double wl[3] = {INFINITY, INFINITY, INFINITY}, wh[3] = {-INFINITY, -INFINITY, -INFINITY};
-	double amax = 0;
+	amax = 0;
 	for (int c = 0; c < 8; c++) {
 		const double p[4] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2], 1.0};
 		double w[4];

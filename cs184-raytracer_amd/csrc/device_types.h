@@ -51,6 +51,9 @@ struct alignas(16) DGeom {
 	// "ray has no direction" (rtbase.h:17-23): every ray must then check this geometry,
 	// even where culling or an early exit would skip it (bvh.cpp, intersect.h).
 	int32_t may_raise;
+	// the world box padded by 2^-20 of its largest coordinate and rounded outward to fp32
+	// (the fp32 world cull, intersect.h world_slab32)
+	float wlo32[3], whi32[3];
 };
 
 struct alignas(16) DMaterial {   // rtbase.h:30-39

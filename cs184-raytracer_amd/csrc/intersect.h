@@ -530,6 +530,63 @@ __device__ __forceinline__ void fetch_node(const DeviceScene& S, int32_t ref, No
 		read_node(S.nodes + ref, r);
 }
 
+// World-space culling in fp32 (RT_WORLD32).  A geometry whose padded world box the ray
+// misses is skipped without its object-space transform; the test only ever skips geometries
+// the exact ray cannot reach, so its precision decides speed, not results.  In fp32:
+//   t = fma(L32, I, -(o32 I +- delta))  per plane, delta = 2^-19 |o|_inf |I_a|
+// The boxes are padded on the host by 2^-20 of their largest coordinate before rounding
+// outward to fp32 (bvh.cpp world_box32), which covers the 2^-22 relative error of I and of
+// L32 I; delta covers the 2^-21 relative error of o32 I (rounding o and the product); the
+// sign of I picks which plane's term is raised, so both slab ends move outward.  Far origins
+// (|o| >= 2^100, fp32 overflow) and NaN directions get infinite delta: never culled here.
+// Replaces round 2's fp64 slab (30 4-cycle instructions per geometry, 12 SGPRs per box in the
+// packet kernels) with 6 fp32 FMAs and the min/max tree (6 SGPRs per box).
+#ifndef RT_WORLD32
+#define RT_WORLD32 0
+#endif
+struct WorldRay32 {
+	float ix, iy, iz;     // I = 1/d, clamped to +-2^60
+	float olx, oly, olz;  // o32 I + delta sign(I): the lower planes' terms
+	float ohx, ohy, ohz;  // o32 I - delta sign(I): the upper planes' terms
+};
+__device__ __forceinline__ WorldRay32 world_ray32(V3 o, V3 d) {
+	WorldRay32 r;
+	const float inv[3] = {__builtin_amdgcn_rcpf(static_cast<float>(d.x)), __builtin_amdgcn_rcpf(static_cast<float>(d.y)),
+	                      __builtin_amdgcn_rcpf(static_cast<float>(d.z))};  // v_rcp_f32: 1 ulp
+	const float o32[3] = {static_cast<float>(o.x), static_cast<float>(o.y), static_cast<float>(o.z)};
+	const float omax = fmaxf(fmaxf(fabsf(o32[0]), fabsf(o32[1])), fabsf(o32[2]));
+	float I[3], lo[3], hi[3];
+#pragma unroll
+	for (int a = 0; a < 3; a++) {
+		// a NaN inverse stays NaN through the clamp's comparisons only if tested first
+		I[a] = (inv[a] == inv[a]) ? fminf(fmaxf(inv[a], -0x1p60f), 0x1p60f) : inv[a];
+		const float oi = o32[a] * I[a];
+		const float delta = (omax < 0x1p100f && I[a] == I[a]) ? 0x1p-19f * omax * fabsf(I[a]) : INFINITY;
+		const float sd = I[a] < 0.0f ? -delta : delta;
+		lo[a] = oi + sd;
+		hi[a] = oi - sd;
+	}
+	r.ix = I[0], r.iy = I[1], r.iz = I[2];
+	r.olx = lo[0], r.oly = lo[1], r.olz = lo[2];
+	r.ohx = hi[0], r.ohy = hi[1], r.ohz = hi[2];
+	return r;
+}
+// lim rounded up to fp32 (+inf stays +inf)
+__device__ __forceinline__ float world_lim32(double lim) {
+	float f = static_cast<float>(lim);
+	if (static_cast<double>(f) < lim) f = __uint_as_float(__float_as_uint(f) + (f >= 0.0f ? 1u : 0xffffffffu));
+	return f;
+}
+template <typename GP>
+__device__ __forceinline__ bool world_slab32(GP G, const WorldRay32& r, float lim) {
+	const float tx0 = fmaf(G->wlo32[0], r.ix, -r.olx), tx1 = fmaf(G->whi32[0], r.ix, -r.ohx);
+	const float ty0 = fmaf(G->wlo32[1], r.iy, -r.oly), ty1 = fmaf(G->whi32[1], r.iy, -r.ohy);
+	const float tz0 = fmaf(G->wlo32[2], r.iz, -r.olz), tz1 = fmaf(G->whi32[2], r.iz, -r.ohz);
+	const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+	const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+	return tmax >= tmin && tmax >= 0.0f && tmin <= lim;
+}
+
 // Mesh::calculateIntNormInObjSpace (geometry.cpp:69-126) with an LBVH in place of the
 // linear scan for large meshes.
 //   kAnyHit = false: the reference's closest face (returns found, Po, No).
@@ -728,13 +785,21 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
                             V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WorkStats& ws) {
 	bool found = false;
 	FaceHit best{-1, 0, 0};
+#if RT_WORLD32
+	const WorldRay32 wr = world_ray32(o, d);
+#else
 	const V3 winv = safe_inv(d);
+#endif
 	check_may_raise(S, d, true, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
-		double tw;
 		PROF_BEGIN(tw0);
+#if RT_WORLD32
+		const bool wb = world_slab32(G, wr, found ? world_lim32(prune_limit(best_dist)) : INFINITY);
+#else
+		double tw;
 		const bool wb = slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw);
+#endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wb) continue;
 		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
@@ -820,15 +885,24 @@ __device__ __forceinline__ double shadow_slab_limit(double dist_light) {
 // The `any` over the geometries, cheap ones first (DeviceScene::shadow_order).
 __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, int32_t* stack,
                          DeviceCounters* ctr, WorkStats& ws) {
+#if RT_WORLD32
+	const WorldRay32 wr = world_ray32(o, d);
+	const float lim = world_lim32(shadow_slab_limit(dist_light));
+#else
 	const V3 winv = safe_inv(d);
 	const double lim = shadow_slab_limit(dist_light);
+#endif
 	check_may_raise(S, d, true, ctr);
 	for (int k = 0; k < S.n_geoms; k++) {
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
-		double tw;
 		PROF_BEGIN(tw0);
+#if RT_WORLD32
+		const bool wb = world_slab32(G, wr, lim);
+#else
+		double tw;
 		const bool wb = slab(G->wlo, G->whi, o, winv, lim, tw);
+#endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (wb && geom_occludes(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
 	}
@@ -973,13 +1047,21 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
                                    WorkStats& ws) {
 	bool found = false;
 	FaceHit best{-1, 0, 0};
+#if RT_WORLD32
+	const WorldRay32 wr = world_ray32(o, d);
+#else
 	const V3 winv = safe_inv(d);
+#endif
 	check_may_raise(S, d, on, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
-		double tw;
 		PROF_BEGIN(tw0);
+#if RT_WORLD32
+		const bool cand = on && world_slab32(G, wr, found ? world_lim32(prune_limit(best_dist)) : INFINITY);
+#else
+		double tw;
 		const bool cand = on && slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw);
+#endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
 		PROF_BEGIN(tx);
@@ -1017,17 +1099,26 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 // Packet form of occluded(): same decisions per lane (see occluded()).
 __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, bool on,
                                 int32_t* wstack, DeviceCounters* ctr, WorkStats& ws) {
-	const V3 winv = safe_inv(d);
 	const bool inf_light = dist_light == INFINITY;
+#if RT_WORLD32
+	const WorldRay32 wr = world_ray32(o, d);
+	const float wlim = world_lim32(shadow_slab_limit(dist_light));
+#else
+	const V3 winv = safe_inv(d);
+#endif
 	bool occ = false;
 	check_may_raise(S, d, on, ctr);
 	if (RT_DIAG_SKIP & 4) return false;
 	for (int k = 0; k < S.n_geoms; k++) {
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
-		double tw;
 		PROF_BEGIN(tw0);
+#if RT_WORLD32
+		const bool cand = on && !occ && world_slab32(G, wr, wlim);
+#else
+		double tw;
 		const bool cand = on && !occ && slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);
+#endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
 #if RT_DIAG_GEOMS
