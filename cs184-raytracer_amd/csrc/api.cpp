@@ -161,6 +161,7 @@ struct Lane {
 	rtamd::ChunkRow* rows_dev = nullptr;  // the chunk's row table (device; FrameGeometry::rows)
 	rtamd::ChunkRow* rows_pin = nullptr;  // its pinned staging (one chunk in flight per lane)
 	int64_t rows_cap = 0;
+	int64_t rows_uploaded = -1;           // rows of the table now on the device (-1: none), = rows_pin[0, n)
 	int level = 0;                        // the level whose counts are awaited
 	std::vector<int64_t> level_n;         // ray counts of the levels known so far
 	std::vector<int> shaded;                        // first level of each shading launch
@@ -189,6 +190,9 @@ struct rt_scene {
 	unsigned long long* stats = nullptr;         // device, kStatShards x kStatStride
 	unsigned long long* summary = nullptr;       // device, ST_COUNT + 1 (k_stats_finish)
 	unsigned long long* summary_host = nullptr;  // pinned mirror
+	// the pinned mirror's device address: k_stats_finish writes the summary straight into host
+	// memory (no copy launch behind it on the call's critical path); null: copy from `summary`
+	unsigned long long* summary_mapped = nullptr;
 	double* out_dev = nullptr;                   // staging for rt_render (f64)
 	int64_t out_capacity = 0;
 	uint8_t* out8_dev = nullptr;                 // staging for rt_render_rgb8
@@ -225,6 +229,9 @@ struct rt_scene {
 	// SIMD each tracing every light in turn leave the GPU latency-bound (one GPU's row share
 	// of a single frame); light-major gives n_lights times the waves, each a shorter chain
 	int64_t light_major_below = 131072;
+	// RTAMD_ONE_STREAM_PIXELS: a replayed chunk of at most this many pixels is issued on one
+	// stream (Render::issue_plan)
+	int64_t one_stream_pixels = (int64_t)1 << 17;
 	int all_lights_for(int first_level, int64_t hits) const {
 		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
 		if (al && ds.n_nonambient > 1 && hits < light_major_below) al = 0;
@@ -536,44 +543,69 @@ struct Render {
 		hipStream_t st = ln.stream;
 		std::vector<hipEvent_t> joins;
 		Plan scratch = pl;
-		for (int L = 0; L < nlev && rc == RT_OK; L++) {
-			const int remaining = depth - L;
-			const bool last = L == nlev - 1;
-			const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
-			step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
-			                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
-			                           last && remaining > 0));
-			launches[0]++;
-			hipEvent_t done = ev(L, 1);
-			step(done ? hipEventRecord(done, st) : hipErrorOutOfMemory);
-			// shading beside the chain only where a later level's tracing can overlap it: a
-			// wait on a not yet signalled event of another queue costs tens of microseconds
-			if (L < direct_levels && rc == RT_OK) {
-				const bool side = L < nlev - 1;
-				hipStream_t q = side ? ln.shade[L % 3] : st;
-				if (side) step(hipStreamWaitEvent(q, done, 0));
+		// A small chunk (a small frame, or a GPU's row share of one) is issued on ONE stream:
+		// the chain, then every level's shading in one batch, then the reductions.  Waits across
+		// queues cost 6-19 us each between kernels of a few us (profiles/round3 timelines); a
+		// large chunk's overlap of shading and tracing is worth them, a small one's is not.
+		if (ln.n0 <= s->one_stream_pixels) {
+			for (int L = 0; L < nlev && rc == RT_OK; L++) {
+				const int remaining = depth - L;
+				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
+				step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
+				                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
+				                           L == nlev - 1 && remaining > 0));
+				launches[0]++;
+			}
+			// levels 0 and 1 alone (their packet forms), the rest together
+			for (int k = 0, e; k < nlev && rc == RT_OK; k = e) {
+				e = k < 2 ? k + 1 : std::min(nlev, k + rtamd::kMaxBatch);
+				std::vector<int> lv;
+				for (int L = k; L < e; L++) lv.push_back(L);
 				scratch.launches[1] = scratch.launches[2] = 0;
-				if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch);
+				rc = launch_shading_dev(ln, lv, st, scratch);
 				launches[1] += scratch.launches[1];
 				launches[2] += scratch.launches[2];
-				if (side) {
-					hipEvent_t sh = ev(L, 4);
-					step(sh ? hipEventRecord(sh, q) : hipErrorOutOfMemory);
-					joins.push_back(sh);
+			}
+		} else {
+			for (int L = 0; L < nlev && rc == RT_OK; L++) {
+				const int remaining = depth - L;
+				const bool last = L == nlev - 1;
+				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
+				step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
+				                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
+				                           last && remaining > 0));
+				launches[0]++;
+				hipEvent_t done = ev(L, 1);
+				step(done ? hipEventRecord(done, st) : hipErrorOutOfMemory);
+				// shading beside the chain only where a later level's tracing can overlap it: a
+				// wait on a not yet signalled event of another queue costs tens of microseconds
+				if (L < direct_levels && rc == RT_OK) {
+					const bool side = L < nlev - 1;
+					hipStream_t q = side ? ln.shade[L % 3] : st;
+					if (side) step(hipStreamWaitEvent(q, done, 0));
+					scratch.launches[1] = scratch.launches[2] = 0;
+					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch);
+					launches[1] += scratch.launches[1];
+					launches[2] += scratch.launches[2];
+					if (side) {
+						hipEvent_t sh = ev(L, 4);
+						step(sh ? hipEventRecord(sh, q) : hipErrorOutOfMemory);
+						joins.push_back(sh);
+					}
 				}
 			}
-		}
-		// the deep levels after the chain, on its own stream (the reductions wait for them)
-		if (rc == RT_OK && nlev > direct_levels) {
-			hipStream_t q = st;
-			std::vector<int> deep;
-			for (int L = direct_levels; L < nlev; L++) deep.push_back(L);
-			for (size_t k = 0, e; k < deep.size() && rc == RT_OK; k = e) {
-				e = std::min(deep.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
-				scratch.launches[1] = scratch.launches[2] = 0;
-				rc = launch_shading_dev(ln, std::vector<int>(deep.begin() + k, deep.begin() + e), q, scratch);
-				launches[1] += scratch.launches[1];
-				launches[2] += scratch.launches[2];
+			// the deep levels after the chain, on its own stream (the reductions wait for them)
+			if (rc == RT_OK && nlev > direct_levels) {
+				hipStream_t q = st;
+				std::vector<int> deep;
+				for (int L = direct_levels; L < nlev; L++) deep.push_back(L);
+				for (size_t k = 0, e; k < deep.size() && rc == RT_OK; k = e) {
+					e = std::min(deep.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
+					scratch.launches[1] = scratch.launches[2] = 0;
+					rc = launch_shading_dev(ln, std::vector<int>(deep.begin() + k, deep.begin() + e), q, scratch);
+					launches[1] += scratch.launches[1];
+					launches[2] += scratch.launches[2];
+				}
 			}
 		}
 		for (hipEvent_t j : joins)
@@ -656,6 +688,7 @@ struct Render {
 			ln.rows_dev = nullptr;
 			ln.rows_pin = nullptr;
 			ln.rows_cap = 0;
+			ln.rows_uploaded = -1;
 			const int64_t cap = std::max<int64_t>(n_rows, 1024);
 			HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ln.rows_dev), cap * sizeof(rtamd::ChunkRow)));
 			HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.rows_pin), cap * sizeof(rtamd::ChunkRow),
@@ -664,22 +697,31 @@ struct Render {
 		}
 		uint64_t h = 1469598103934665603ull;
 		int64_t q = 0;
+		// the table is rewritten in place; a render call repeating the lane's previous chunk (the
+		// same rows into the same buffers: a frame rendered again) finds it already on the device
+		// and skips the copy (a blit launch on the chain's critical path)
+		bool same = ln.rows_uploaded == n_rows;
 		for (const Segment& sg : segs) {
 			const Job& job = *sg.job;
 			const rt_render_params* p = job.p;
 			for (int64_t k = 0; k < sg.rows; k++, q++) {
 				const int64_t ord = sg.r0 + k;  // the job's selected-row ordinal: its output row
-				rtamd::ChunkRow& r = ln.rows_pin[q];
+				rtamd::ChunkRow r{};
 				r.row = selected_row(p, ord);
 				r.pad = 0;
 				r.out = job.out_rgb_dev ? job.out_rgb_dev + ord * job.W * 3 : nullptr;
 				r.out8 = job.out_rgb8_dev ? job.out_rgb8_dev + ord * job.W * 3 : nullptr;
+				rtamd::ChunkRow& dst = ln.rows_pin[q];
+				same = same && dst.row == r.row && dst.out == r.out && dst.out8 == r.out8;
+				dst = r;
 				h = (h ^ static_cast<uint32_t>(r.row)) * 1099511628211ull;
 			}
 		}
 		ln.rows_hash = h;
-		HIP_TRY(hipMemcpyAsync(ln.rows_dev, ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow), hipMemcpyHostToDevice,
-		                       ln.stream));
+		if (!same)
+			HIP_TRY(hipMemcpyAsync(ln.rows_dev, ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow), hipMemcpyHostToDevice,
+			                       ln.stream));
+		ln.rows_uploaded = n_rows;
 		return RT_OK;
 	}
 
@@ -1072,6 +1114,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
 	if (const char* lm = std::getenv("RTAMD_LIGHT_MAJOR_BELOW")) s->light_major_below = std::atoll(lm);
+	if (const char* os = std::getenv("RTAMD_ONE_STREAM_PIXELS")) s->one_stream_pixels = std::atoll(os);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
 	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);
@@ -1126,6 +1169,12 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	s->summary = static_cast<unsigned long long*>(sm);
 	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->summary_host), sizeof(unsigned long long) * (rtamd::ST_COUNT + 1),
 	                      hipHostMallocDefault));
+	{
+		void* mapped = nullptr;
+		if (!std::getenv("RTAMD_SUMMARY_COPY") && hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
+			s->summary_mapped = static_cast<unsigned long long*>(mapped);
+		(void)hipGetLastError();
+	}
 	// statistics and the error word start cleared; k_stats_finish clears them after each render
 	HIP_TRY(hipMemset(s->ctr, 0, sizeof(rtamd::DeviceCounters)));
 	HIP_TRY(hipMemset(s->stats, 0, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
@@ -1181,6 +1230,7 @@ void reset_after_error(rt_scene* s) {
 	for (auto& ln : s->lanes) {
 		ln->phase = Lane::IDLE;
 		ln->segs.clear();
+		ln->rows_uploaded = -1;
 		ln->level = 0;
 		ln->level_n.clear();
 		ln->shaded.clear();
@@ -1332,6 +1382,23 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, s->batch_balance, s->chunks_per_lane);
 	size_t next_chunk = 0;
 	std::unique_ptr<rtamd::MarkerRange> trace_range(new rtamd::MarkerRange("rtamd: trace (levels, shading, output)"));
+	// The statistics reduction is queued on the caller's stream, behind every lane's last
+	// chunk, as soon as all of the call's launches are issued, not after the host has seen
+	// them complete: a launch onto an idle GPU takes ~30 us to start, which is a third of a
+	// small frame (profiles/round3 marker trace)
+	bool stats_issued = false;
+	auto issue_stats = [&]() -> int {
+		for (size_t k = 0; k < n_lanes; k++) HIP_TRY(hipStreamWaitEvent(caller, s->lanes[k]->chunk_done, 0));
+		if (s->summary_mapped) {
+			HIP_TRY(rtamd::launch_stats_finish(s->stats, s->ctr, s->summary_mapped, caller));
+		} else {
+			HIP_TRY(rtamd::launch_stats_finish(s->stats, s->ctr, s->summary, caller));
+			HIP_TRY(hipMemcpyAsync(s->summary_host, s->summary, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1),
+			                       hipMemcpyDeviceToHost, caller));
+		}
+		stats_issued = true;
+		return RT_OK;
+	};
 	for (;;) {
 		bool busy = false;
 		for (size_t k = 0; k < n_lanes; k++) {
@@ -1350,6 +1417,11 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 			rc = ln.phase == Lane::TRACING ? R.on_counts(ln) : R.on_done(ln);
 			if (rc) return rc;
 		}
+		if (!stats_issued && next_chunk >= chunks.size()) {
+			bool issued = true;  // every lane idle or with its last chunk fully queued
+			for (size_t k = 0; k < n_lanes; k++) issued = issued && s->lanes[k]->phase != Lane::TRACING;
+			if (issued && (rc = issue_stats())) return rc;
+		}
 		if (progress && progress->fn && progress->done < progress->total) {
 			const double t = now_s();
 			if (t - progress->last >= 0.1) {  // scene.cpp:41-44 polls every 100 ms
@@ -1361,11 +1433,9 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	}
 	trace_range.reset();
 	rtamd::MarkerRange stats_range("rtamd: statistics read-back");
-	// all lanes' work is complete (their events were observed): reduce the statistics on the
-	// device and read back one small summary
-	HIP_TRY(rtamd::launch_stats_finish(s->stats, s->ctr, s->summary, caller));
-	HIP_TRY(hipMemcpyAsync(s->summary_host, s->summary, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1),
-	                       hipMemcpyDeviceToHost, caller));
+	// all lanes' work is complete (their events were observed); the statistics reduction is
+	// queued behind it (above) and one small summary read back
+	if (!stats_issued && (rc = issue_stats())) return rc;
 	HIP_TRY(hipStreamSynchronize(caller));
 	const unsigned long long* sum = s->summary_host;
 	if (sum[rtamd::ST_COUNT] == rtamd::DERR_PLAN) return kPlanMiss;

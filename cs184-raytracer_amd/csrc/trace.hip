@@ -779,6 +779,9 @@ __global__ void k_stats_finish(unsigned long long* stats, DeviceCounters* ctr, u
 		summary[t] = static_cast<unsigned long long>(ctr->error);
 		ctr->error = 0;
 	}
+	// summary may be pinned host memory (api.cpp summary_mapped): visible to the host at
+	// system scope before the kernel completes
+	__threadfence_system();
 }
 
 __global__ void k_normalize(int64_t n_values, double* rgb, double rcp, uint8_t* out8) {

@@ -10,6 +10,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # tests that exercise it set it explicitly (test_gpu_fuzz odd seeds, knob tests, the bench
 # batch test).
 os.environ.setdefault("RTAMD_LIGHT_MAJOR_BELOW", "0")
+# likewise the one-stream issue of small replayed chunks (api.cpp one_stream_pixels): off by
+# default so the multi-stream schedule stays covered; odd fuzz seeds and a knob test run it
+os.environ.setdefault("RTAMD_ONE_STREAM_PIXELS", "0")
 for p in (os.path.join(REPO, "cs184-raytracer_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

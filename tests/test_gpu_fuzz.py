@@ -103,6 +103,7 @@ _W, _H = (int(v) for v in os.environ.get("RTAMD_FUZZ_SIZE", "56x40").split("x"))
 def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
     # odd seeds: the production light-major threshold (every launch here is below it)
     monkeypatch.setenv("RTAMD_LIGHT_MAJOR_BELOW", "131072" if seed % 2 else "0")
+    monkeypatch.setenv("RTAMD_ONE_STREAM_PIXELS", "131072" if seed % 2 else "0")
     path, bdepth, io = random_scene(seed, tmp_path)
     w, h = _W, _H
     try:
@@ -116,9 +117,13 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
         s.close()
         return
     s = gpu.load_scene(path)
-    got = s.renderScene(options=gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth,
-                                             intersectionOnly_=io))
+    opts = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth, intersectionOnly_=io)
+    got = s.renderScene(options=opts)
     st = s.last_stats
+    if seed % 2:  # again: the first render traced host-driven and built a launch plan; this one replays it
+        again = s.renderScene(options=opts)
+        assert np.array_equal(np.ascontiguousarray(again).view(np.uint64), np.ascontiguousarray(got).view(np.uint64))
+        assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (st.trace_rays, st.shadow_rays)
     s.close()
     g, r = np.ascontiguousarray(got).view(np.uint64), np.ascontiguousarray(want).view(np.uint64)
     diff = int((g != r).any(axis=2).sum())
