@@ -267,6 +267,43 @@ void world_box_impl(const Geometry& g, const double lo[3], const double hi[3], D
 	}
 }
 
+// World-space bounding sphere of a sphere geometry (intersect.h sphere_cull): centre fwd(c),
+// radius sqrt(rr) * sigma, sigma an upper bound of the largest singular value of fwd's 3x3
+// part (Gershgorin on M^T M: exact for a rotation times a uniform scale), padded relatively by
+// 1e-6 and by 1e-9 of the centre's magnitude.  Only ever used to skip the geometry.
+void world_sphere(const Geometry& g, DGeom& d) {
+	d.wr = -1.0;
+	bool finite = std::isfinite(g.det) && g.det != 0;
+	for (int i = 0; i < 3; i++)
+		for (int j = 0; j < 4; j++) finite = finite && std::isfinite(g.fwd.m[i][j]);
+	if (!finite || !(d.rr >= 0) || !std::isfinite(d.rr)) return;
+	double A[3][3];
+	for (int i = 0; i < 3; i++)
+		for (int j = 0; j < 3; j++) {
+			A[i][j] = 0;
+			for (int k = 0; k < 3; k++) A[i][j] += g.fwd.m[k][i] * g.fwd.m[k][j];
+		}
+	double lam = 0;
+	for (int i = 0; i < 3; i++) {
+		double r = A[i][i];
+		for (int j = 0; j < 3; j++)
+			if (j != i) r += std::fabs(A[i][j]);
+		lam = std::max(lam, r);
+	}
+	const double c4[4] = {g.center[0], g.center[1], g.center[2], 1.0};
+	double w[4];
+	affine_apply(g.fwd, c4, w);
+	double cmax = 0;
+	for (int k = 0; k < 3; k++) {
+		d.wc[k] = w[k];
+		cmax = std::max(cmax, std::fabs(w[k]));
+	}
+	const double r = std::sqrt(d.rr) * std::sqrt(lam) * (1.0 + 1e-6) + 1e-9 * cmax + 1e-300;
+	if (!std::isfinite(r) || !std::isfinite(cmax)) return;
+	d.wr = r;
+	d.wr2 = r * r * (1.0 + 1e-12);
+}
+
 // True unless every unit world direction is certain to keep a component above 1e-12 in
 // object space: |inv d| >= sigma_min(inv) >= |det(inv)| / ||inv||_F^2 (3x3 part).
 bool direction_may_vanish(const Affine& inv) {
@@ -382,6 +419,7 @@ FlatScene flatten_scene(const Scene& s) {
 			const double lo[3] = {g.center[0] - rad, g.center[1] - rad, g.center[2] - rad};
 			const double hi[3] = {g.center[0] + rad, g.center[1] + rad, g.center[2] + rad};
 			world_box(g, lo, hi, d);
+			world_sphere(g, d);
 			fs.geoms.push_back(d);
 			continue;
 		}

@@ -54,6 +54,9 @@ struct alignas(16) DGeom {
 	// the world box padded by 2^-20 of its largest coordinate and rounded outward to fp32
 	// (the fp32 world cull, intersect.h world_slab32)
 	float wlo32[3], whi32[3];
+	// spheres: a world-space bounding sphere (centre, radius and its square, padded; radius
+	// -1: none) for the cull of intersect.h sphere_cull (tighter than the box for a sphere)
+	double wc[3], wr, wr2;
 };
 
 struct alignas(16) DMaterial {   // rtbase.h:30-39

@@ -530,6 +530,35 @@ __device__ __forceinline__ void fetch_node(const DeviceScene& S, int32_t ref, No
 		read_node(S.nodes + ref, r);
 }
 
+// Bounding-sphere cull of sphere geometries (RT_SPHERE_CULL), instead of their world box.
+// With v = wc - o and b = v.d (d unit), a ray can meet the padded world sphere (wc, wr) on
+// [0, lim] only if its squared distance to the centre line q = v.v - b^2 <= wr^2 and
+// -wr <= b <= lim + wr.  The fp64 rounding of v, b and q errs by < 2^-47 |v|^2 in q and
+// < 2^-50 |v| in b; the slack 2^-40 v.v on q and eo = 2^-30 |o|_1 on b (with the host's
+// 1e-9 |wc| in wr) exceed both, so the test never drops a sphere the exact ray reaches.
+// A sphere's box admits rays through its corners (1.9x the sphere's volume); each one
+// the sphere test rejects saves an object-space transform, normalisation and quadratic.
+#ifndef RT_SPHERE_CULL
+#define RT_SPHERE_CULL 0
+#endif
+__device__ __forceinline__ double sphere_cull_slack(V3 o) { return 0x1p-30 * ((fabs(o.x) + fabs(o.y)) + fabs(o.z)); }
+template <typename GP>
+__device__ __forceinline__ bool sphere_cull(GP G, V3 o, V3 d, double lim) {
+	const double eo = sphere_cull_slack(o);  // per test, not held per ray (register pressure)
+	const double vx = G->wc[0] - o.x, vy = G->wc[1] - o.y, vz = G->wc[2] - o.z;
+	const double b = (vx * d.x + vy * d.y) + vz * d.z;
+	const double vv = (vx * vx + vy * vy) + vz * vz;
+	const double rt = G->wr + eo;
+	return vv - b * b <= G->wr2 + 0x1p-40 * vv && b >= -rt && b <= lim + rt;
+}
+// The world cull of geometry G: its bounding sphere (spheres) or its padded box
+template <typename GP>
+__device__ __forceinline__ bool world_cull(GP G, V3 o, V3 d, V3 winv, double lim) {
+	if (RT_SPHERE_CULL && G->kind == DGEOM_SPHERE && G->wr >= 0.0) return sphere_cull(G, o, d, lim);
+	double tw;
+	return slab(G->wlo, G->whi, o, winv, lim, tw);
+}
+
 // World-space culling in fp32 (RT_WORLD32).  A geometry whose padded world box the ray
 // misses is skipped without its object-space transform; the test only ever skips geometries
 // the exact ray cannot reach, so its precision decides speed, not results.  In fp32:
@@ -797,8 +826,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 #if RT_WORLD32
 		const bool wb = world_slab32(G, wr, found ? world_lim32(prune_limit(best_dist)) : INFINITY);
 #else
-		double tw;
-		const bool wb = slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw);
+		const bool wb = world_cull(G, o, d, winv, found ? prune_limit(best_dist) : INFINITY);
 #endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wb) continue;
@@ -900,8 +928,7 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 #if RT_WORLD32
 		const bool wb = world_slab32(G, wr, lim);
 #else
-		double tw;
-		const bool wb = slab(G->wlo, G->whi, o, winv, lim, tw);
+		const bool wb = world_cull(G, o, d, winv, lim);
 #endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (wb && geom_occludes(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
@@ -1059,8 +1086,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 #if RT_WORLD32
 		const bool cand = on && world_slab32(G, wr, found ? world_lim32(prune_limit(best_dist)) : INFINITY);
 #else
-		double tw;
-		const bool cand = on && slab(G->wlo, G->whi, o, winv, found ? prune_limit(best_dist) : INFINITY, tw);
+		const bool cand = on && world_cull(G, o, d, winv, found ? prune_limit(best_dist) : INFINITY);
 #endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
@@ -1116,8 +1142,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 #if RT_WORLD32
 		const bool cand = on && !occ && world_slab32(G, wr, wlim);
 #else
-		double tw;
-		const bool cand = on && !occ && slab(G->wlo, G->whi, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6), tw);
+		const bool cand = on && !occ && world_cull(G, o, d, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6));
 #endif
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;

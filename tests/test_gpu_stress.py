@@ -182,3 +182,23 @@ def test_facing_pretest_vertex_normals(gpu, oracle, tmp_path, mode):
             "ltp   0 0 -5 0.3 0.3 0.3\n" + MAT_SHINY + 'obj   "nsoup.obj"\n' + MAT_GLASS +
             "sph   0.3 -0.2 1.5 0.5\n" + MAT_MIRROR + "sph   -1.6 0.9 -1.5 0.7\n")
     check(gpu, oracle, scene(tmp_path, "nsoup_" + mode, body), w=64, h=48, bdepth=4, bits=True)
+
+
+CAM6 = "cam 0 0 6  -2 -2 2  2 -2 2  -2 2 2  2 2 2"
+
+
+@pytest.mark.parametrize("xf,cam", [
+    ("xfs 3 0.2 1\nxfr 30 45 10", CAM6), ("xfr 0 0 37\nxfs 0.05 4 0.5", CAM6),
+    ("xfr 80 0.1 0\nxfs 1 1 1e-3", CAM6), ("xfr 60 20 0\nxfs 1 1 0.02", CAM6),
+    ("xft 1e4 -2e4 3e4\nxfs 2 2 2", "cam 1e4 -2e4 3.0008e4  9996 -20004 3.0004e4  10004 -20004 3.0004e4  9996 -19996 3.0004e4  "
+                                    "10004 -19996 3.0004e4"),
+    ("xfs 1e-3 1e-3 1e-3", "cam 0 0 0.006  -0.002 -0.002 0.002  0.002 -0.002 0.002  -0.002 0.002 0.002  0.002 0.002 0.002")])
+def test_sphere_bounding_cull_silhouettes(gpu, oracle, tmp_path, xf, cam):
+    """The bounding-sphere cull of sphere geometries (intersect.h sphere_cull, round 3) may
+    skip a sphere only when the exact ray cannot reach it.  Ellipsoids under anisotropic
+    scales and rotations (flattened to discs), far translations and tiny scales, framed so
+    that many primary, mirror and shadow rays graze their silhouettes, must render bit for
+    bit as the oracle (rows of mirror and glass spheres reflecting each other)."""
+    rows = [f"sph {1.5 * i - 1.5:.3f} {1.5 * j - 1.5:.3f} 0 0.7" for i in range(3) for j in range(3)]
+    body = cam + "\n" + LIGHTS + xf + "\n" + MAT_MIRROR + "\n".join(rows[:5]) + "\n" + MAT_GLASS + "\n".join(rows[5:]) + "\n"
+    check(gpu, oracle, scene(tmp_path, "ellipsoids", body), w=96, h=72, bdepth=4, bits=True)
