@@ -401,6 +401,63 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	return kAnyHit && dist < any_limit;
 }
 
+// The wave-packet form of test_face (RT_PRED_FACE): the same decisions, but each lane's
+// early exits become a running predicate and the wave leaves only when no lane is left
+// (a wave-uniform branch).  The branchy form pays exec-mask bookkeeping (s_and_saveexec,
+// s_cbranch_execz, the join) at every exit of every face test, in a kernel whose
+// instruction stream is as much scalar as vector; here a lane that has failed just
+// computes along, its results never selected.  Divisions of failed lanes may see D = 0
+// (inf/NaN, discarded).  Returns, per lane, kAnyHit && the face passes within any_limit.
+#ifndef RT_PRED_FACE
+#define RT_PRED_FACE 1
+#endif
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
+template <bool kAnyHit>
+__device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn,
+                                               bool reverse, double any_limit, MeshBest& best, WorkStats& ws,
+                                               bool on) {
+	if (on) ws.inc<W_TRIS>();
+	const auto F = uniform_ptr(S.fgeo) + f;
+	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	const int32_t id = F->id;
+	const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
+	asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
+	             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
+	bool ok = on && !(RT_FACING && facing_rejects(c0, c1, c2, tau, d, reverse));
+	if (!wave_any(ok)) return false;
+	const V3 rhs = o - p0;
+	const double D = det3(va, vb, nd);
+	const double Da = det3(rhs, vb, nd);
+	ok = ok && D != 0 && !quotient_surely_negative(Da, D) && !quotient_surely_above(Da, D, 1.0);
+	if (!wave_any(ok)) return false;
+	const double a = Da / D;
+	const double Db = det3(va, rhs, nd);
+	ok = ok && a >= 0 && a <= 1 && !quotient_surely_negative(Db, D) && !quotient_surely_above(Db, D, 1.0);
+	if (!wave_any(ok)) return false;
+	const double b = Db / D;
+	const double Dt = det3(va, vb, rhs);
+	// dist = t * dn with dn = |d|_3 within a few ulps of 1: t > 1.001 * best * 1.001 cannot win
+	const bool beyond = best.dist < INFINITY && best.dist >= 0x1p-900 && quotient_surely_above(Dt, D, best.dist * 1.001);
+	ok = ok && b >= 0 && a + b <= 1 && !quotient_surely_negative(Dt, D) && !beyond;
+	if (!wave_any(ok)) return false;
+	const double t = Dt / D;
+	const double dist = t * dn;
+	ok = ok && t >= 0 && (dist < best.dist || (dist == best.dist && id < best.id));
+	if (!wave_any(ok)) return false;
+	if (ok) ws.inc<W_CANDS>();
+	const V3 tn = face_normal<true>(S, f, a, b);
+	const bool front = dot4z(tn, d) < 0;
+	ok = ok && !(!front ^ reverse);
+	if (ok) {
+		best.dist = dist;
+		best.face = f;
+		best.id = id;
+		best.a = a;
+		best.b = b;
+	}
+	return kAnyHit && ok && dist < any_limit;
+}
+
 // Slab test of a padded box; conservative: the interval is widened by a relative 1e-9.
 template <typename P>
 __device__ __forceinline__ bool slab(P lo, P hi, V3 o, V3 inv, double tlimit, double& tnear) {
@@ -946,7 +1003,6 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 // test there (pruning and tie-breaks are per lane), it may only test a few more.
 // Callers must reach these functions with all lanes (inactive lanes pass on = false).
 
-__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 // A value every lane holds equally (node and face indices of the packet traversal): read
 // from the first lane, so the compiler keeps it in an SGPR and the node/face records at
 // that index are fetched with scalar loads instead of 64 identical vector loads.
@@ -967,11 +1023,15 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	if (wave_any(live)) {
 		if (G->bvh_root < 0) {
 			PROF_BEGIN(tf);
-			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++)
-				if (live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
-					settled = true;
-					live = false;
-				}
+			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++) {
+				bool hitf;
+				if (RT_PRED_FACE)
+					hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws, live);
+				else
+					hitf = live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws);
+				settled = settled || hitf;
+				live = live && !hitf;
+			}
 				PROF_END(ws, PH_FACES, tf);
 		} else if (!(RT_DIAG_SKIP & 1)) {
 			if (live) ws.inc<W_ENTRIES>();
@@ -1041,12 +1101,17 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					if (!want) continue;
 					PROF_BEGIN(tf);
 					const int32_t f0 = fbase + cf;
-					for (int32_t f = f0; f < f0 + cc; f++)
-						if (__builtin_amdgcn_inverse_ballot_w64(want) && live &&
-						    test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
-							settled = true;
-							live = false;
-						}
+					for (int32_t f = f0; f < f0 + cc; f++) {
+						bool hitf;
+						if (RT_PRED_FACE)
+							hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws,
+							                               __builtin_amdgcn_inverse_ballot_w64(want) && live);
+						else
+							hitf = __builtin_amdgcn_inverse_ballot_w64(want) && live &&
+							       test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws);
+						settled = settled || hitf;
+						live = live && !hitf;
+					}
 					lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 					tested = true;
 					PROF_END(ws, PH_FACES, tf);
