@@ -411,20 +411,37 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 #ifndef RT_PRED_FACE
 #define RT_PRED_FACE 1
 #endif
+#ifndef RT_PRED_FACE_LANE
+#define RT_PRED_FACE_LANE 0
+#endif
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
-template <bool kAnyHit>
+// kUniform false (RT_PRED_FACE_LANE): the per-lane LBVH search's form, each lane on a face
+// of its own leaf (f must index a face for every lane, `on` or not); the vertices are
+// fetched after the facing pre-test, as in test_face.
+template <bool kAnyHit, bool kUniform = true>
 __device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn,
                                                bool reverse, double any_limit, MeshBest& best, WorkStats& ws,
                                                bool on) {
 	if (on) ws.inc<W_TRIS>();
-	const auto F = uniform_ptr(S.fgeo) + f;
-	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-	const int32_t id = F->id;
-	const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
-	asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
-	             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
-	bool ok = on && !(RT_FACING && facing_rejects(c0, c1, c2, tau, d, reverse));
-	if (!wave_any(ok)) return false;
+	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
+	V3 p0, va, vb;
+	int32_t id;
+	bool ok;
+	if constexpr (kUniform) {
+		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+		id = F->id;
+		const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
+		asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
+		             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
+		ok = on && !(RT_FACING && facing_rejects(c0, c1, c2, tau, d, reverse));
+		if (!wave_any(ok)) return false;
+	} else {
+		ok = on && !(RT_FACING && face_facing_rejects(F, d, reverse));
+		if (!wave_any(ok)) return false;
+		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+		id = F->id;
+		asm volatile("" ::"v"(id));
+	}
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	const double Da = det3(rhs, vb, nd);
@@ -445,7 +462,7 @@ __device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, 
 	ok = ok && t >= 0 && (dist < best.dist || (dist == best.dist && id < best.id));
 	if (!wave_any(ok)) return false;
 	if (ok) ws.inc<W_CANDS>();
-	const V3 tn = face_normal<true>(S, f, a, b);
+	const V3 tn = face_normal<kUniform>(S, f, a, b);
 	const bool front = dot4z(tn, d) < 0;
 	ok = ok && !(!front ^ reverse);
 	if (ok) {
@@ -722,6 +739,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		// still walking inner nodes postpones it (`leaf`) and keeps walking, so fewer lanes
 		// idle in either phase.  Any visiting order selects the same face (test_face).
 		int32_t leaf = -1;
+		bool occluded = false;  // RT_PRED_FACE_LANE: an any-hit face passed within any_limit
 		while (ref != -1 || leaf != -1) {
 			PROF_BEGIN(tn);
 			while (ref >= 0) {
@@ -766,6 +784,29 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 			}
 			// the postponed leaf, then a leaf the walk stopped on
 			PROF_BEGIN(tf);
+#if RT_PRED_FACE_LANE
+			// the lanes holding a leaf test face k of it together, k up to the wave's largest
+			// leaf (test_face_pred); an occluded lane leaves the search (ref = leaf = -1)
+			while (wave_any(leaf != -1)) {
+				const int32_t code = leaf != -1 ? -2 - leaf : 0;
+				const int32_t fb = G->face_begin + (code >> 3);
+				int32_t cnt = code & 7;
+				for (int32_t k = 0; wave_any(k < cnt); k++) {
+					const bool on = k < cnt;
+					if (test_face_pred<kAnyHit, false>(S, on ? fb + k : fb, o, d, nd, dn, reverse, any_limit, best,
+					                                   ws, on)) {
+						occluded = true;
+						cnt = 0;
+						ref = -1;
+					}
+				}
+				leaf = -1;
+				if (ref <= -2) {
+					leaf = ref;
+					ref = pop();
+				}
+			}
+#else
 			while (leaf != -1) {
 				const int32_t code = -2 - leaf;
 				const int32_t f0 = G->face_begin + (code >> 3), f1 = f0 + (code & 7);
@@ -781,8 +822,13 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 					ref = pop();
 				}
 			}
+#endif
 			lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 			PROF_END(ws, PH_FACES, tf);
+		}
+		if (occluded) {
+			settled = true;
+			return true;
 		}
 	}
 	found_dist = best.dist;
