@@ -1823,6 +1823,35 @@ int rt_debug_valu_calibration(int device, int iters) {
 	return RT_OK;
 }
 
+// Diagnostic (not in rtamd.h): k_valu_peak of one instruction kind (trace.hip kValuKinds) at
+// `waves` waves per SIMD, timed with events after a warm-up launch; *ms = kernel time.  The
+// kernel issues 256 * waves * 4 waves * iters * 128 instructions.
+int rt_debug_valu_rate(int device, int kind, int waves, int iters, double* ms) {
+	if (!ms || kind < 0 || waves < 1 || waves > 8 || iters < 1) return fail(RT_ERR_ARG, "bad calibration arguments");
+	HIP_TRY(hipSetDevice(device));
+	struct Res {
+		void* p = nullptr;
+		hipEvent_t e0 = nullptr, e1 = nullptr;
+		~Res() {
+			if (p) (void)hipFree(p);
+			if (e0) (void)hipEventDestroy(e0);
+			if (e1) (void)hipEventDestroy(e1);
+		}
+	} r;
+	HIP_TRY(hipMalloc(&r.p, 64));
+	HIP_TRY(hipEventCreate(&r.e0));
+	HIP_TRY(hipEventCreate(&r.e1));
+	HIP_TRY(rtamd::launch_valu_peak(std::max(1, iters / 4), kind, waves, r.p, nullptr));  // warm-up (clocks)
+	HIP_TRY(hipEventRecord(r.e0, nullptr));
+	HIP_TRY(rtamd::launch_valu_peak(iters, kind, waves, r.p, nullptr));
+	HIP_TRY(hipEventRecord(r.e1, nullptr));
+	HIP_TRY(hipEventSynchronize(r.e1));
+	float f = 0;
+	HIP_TRY(hipEventElapsedTime(&f, r.e0, r.e1));
+	*ms = f;
+	return RT_OK;
+}
+
 // Diagnostic (not in rtamd.h): the scene's next render fails after `launches` more
 // closest-hit launches, as a device failure in the middle of a render would (tests of the
 // error path: the render after it must be complete and exact).  -1 disables.

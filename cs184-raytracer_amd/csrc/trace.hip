@@ -830,15 +830,86 @@ __global__ void k_stream_read(const T* __restrict__ p, int64_t n, unsigned long 
 // VALU issue calibration (tools/valu_calibration.py, profiles/): every wave runs `iters`
 // rounds of 32 independent chains, unrolled 4x (128 instructions per round, nothing else
 // in the loop but the counter), on every CU at W waves per SIMD (grid 256 W blocks of 4
-// waves).  K selects the instruction: 0 v_fma_f32, 1 v_pk_fma_f32 (two f32 FMAs per lane),
-// 2 v_fma_f64.  Operands are the chain's own register and inline constants (0.5, 1.0: the
-// chains converge to 2, never to a denormal or infinity), so no operand read limits issue.
-// rocprofv3 (SQ_INSTS_VALU, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE + kernel trace) turns it
-// into cycles per wave64 instruction per SIMD and the shader clock.
+// waves).  K selects the instruction (kValuKinds): 0 v_fma_f32, 1 v_pk_fma_f32 (two f32
+// FMAs per lane), 2 v_fma_f64, then the other instructions the traversal kernels are made
+// of (--mix: 64-bit add/mul/max/compare/move, 32-bit select/integer add/move/compare, the
+// f64 reciprocal; 13-16: v_cndmask_b32 with its mask in an SGPR pair set by a ballot, in
+// VCC set by a compare before the loop, with two vector sources, and v_cmp_gt_f64 into an
+// SGPR pair; 17-18: v_cndmask_b32 of two vector sources under VCC, VOP2 and VOP3 encodings;
+// 19-25: the f64 division's v_div_fmas / v_div_scale / v_div_fixup, v_addc_co_u32 (VOP2,
+// carry in VCC), v_readlane_b32 / v_writelane_b32 (SGPR spill traffic), v_sqrt_f64).
+// Operands are the chain's own register and inline constants (the chains
+// stay finite and normal), so no operand read limits issue.  rocprofv3 (SQ_INSTS_VALU,
+// SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE + kernel trace), or the events of
+// rt_debug_valu_rate, turn it into cycles per wave64 instruction per SIMD.
+constexpr int kValuKinds = 26;
+template <int K>
+__device__ __forceinline__ void valu_op(float& x) {
+	if constexpr (K == 0) asm volatile("v_fma_f32 %0, %0, 0.5, 1.0" : "+v"(x));
+	if constexpr (K == 7) asm volatile("v_cndmask_b32 %0, 1.0, %0, vcc" : "+v"(x));
+	if constexpr (K == 8) asm volatile("v_add_u32 %0, 1, %0" : "+v"(x));
+	if constexpr (K == 9) asm volatile("v_mov_b32 %0, %0" : "+v"(x));
+	if constexpr (K == 10) asm volatile("v_cmp_gt_f32 vcc, 1.0, %0" : "+v"(x)::"vcc");
+}
+template <int K>
+__device__ __forceinline__ void valu_op(double& x) {
+	if constexpr (K == 2) asm volatile("v_fma_f64 %0, %0, 0.5, 1.0" : "+v"(x));
+	if constexpr (K == 3) asm volatile("v_add_f64 %0, %0, 1.0" : "+v"(x));
+	if constexpr (K == 4) asm volatile("v_mul_f64 %0, %0, 1.0" : "+v"(x));
+	if constexpr (K == 5) asm volatile("v_max_f64 %0, %0, 1.0" : "+v"(x));
+	if constexpr (K == 6) asm volatile("v_cmp_gt_f64 vcc, 1.0, %0" : "+v"(x)::"vcc");
+	if constexpr (K == 11) asm volatile("v_mov_b64 %0, %0" : "+v"(x));
+	if constexpr (K == 12) asm volatile("v_rcp_f64 %0, %0" : "+v"(x));
+}
 template <int K>
 __global__ void __launch_bounds__(256) k_valu_peak(int iters, float seed, float* sink) {
+	if constexpr (K >= 13) {
+		// select / compare forms with an explicit mask
+		constexpr int kChains = 32;
+		const unsigned long long mask = __ballot(threadIdx.x & 1);
+		float a[kChains];
+		double b[kChains];
+#pragma unroll
+		for (int k = 0; k < kChains; k++) a[k] = seed + threadIdx.x + k, b[k] = a[k];
+		const float y = seed * 3;
+		if constexpr (K == 14 || K == 17 || K == 18 || K == 19 || K == 22) asm volatile("v_cmp_gt_f32 vcc, 1.0, %0" ::"v"(y) : "vcc");
+		for (int i = 0; i < iters; i++) {
+#pragma unroll
+			for (int u = 0; u < 4; u++)
+#pragma unroll
+				for (int k = 0; k < kChains; k++) {
+					if constexpr (K == 13) asm volatile("v_cndmask_b32_e64 %0, 1.0, %0, %1" : "+v"(a[k]) : "s"(mask));
+					if constexpr (K == 14) asm volatile("v_cndmask_b32 %0, 1.0, %0, vcc" : "+v"(a[k]));
+					if constexpr (K == 15) asm volatile("v_cndmask_b32_e64 %0, %1, %0, %2" : "+v"(a[k]) : "v"(y), "s"(mask));
+					if constexpr (K == 17) asm volatile("v_cndmask_b32_e32 %0, %1, %0, vcc" : "+v"(a[k]) : "v"(y));
+					if constexpr (K == 18) asm volatile("v_cndmask_b32_e64 %0, %1, %0, vcc" : "+v"(a[k]) : "v"(y));
+					if constexpr (K == 19) asm volatile("v_div_fmas_f64 %0, %0, 1.0, 1.0" : "+v"(b[k])::"vcc");
+					if constexpr (K == 20) asm volatile("v_div_scale_f64 %0, vcc, %0, %0, 1.0" : "+v"(b[k])::"vcc");
+					if constexpr (K == 21) asm volatile("v_div_fixup_f64 %0, %0, 1.0, 1.0" : "+v"(b[k]));
+					if constexpr (K == 22) asm volatile("v_addc_co_u32_e32 %0, vcc, 0, %0, vcc" : "+v"(a[k])::"vcc");
+					if constexpr (K == 23) {
+						uint32_t t;
+						asm volatile("v_readlane_b32 %0, %1, 5" : "=s"(t) : "v"(a[k]));
+						asm volatile("" ::"s"(t));
+					}
+					if constexpr (K == 24) asm volatile("v_writelane_b32 %0, %1, 3" : "+v"(a[k]) : "s"((uint32_t)mask));
+					if constexpr (K == 25) asm volatile("v_sqrt_f64 %0, %0" : "+v"(b[k]));
+					if constexpr (K == 16) {
+						unsigned long long m;
+						asm volatile("v_cmp_gt_f64_e64 %0, 1.0, %1" : "=s"(m) : "v"(b[k]));
+						asm volatile("" ::"s"(m));
+					}
+				}
+		}
+		float acc = 0;
+#pragma unroll
+		for (int k = 0; k < kChains; k++) acc += a[k] + (float)b[k];
+		if (acc == -1.0f) sink[0] = acc;  // keeps the chains; never true
+		return;
+	}
 	constexpr int kChains = 32;
-	using T = typename std::conditional<K == 2, double, float>::type;
+	constexpr bool k64 = K == 2 || K == 3 || K == 4 || K == 5 || K == 6 || K == 11 || K == 12;
+	using T = typename std::conditional<k64, double, float>::type;
 	constexpr int kLanes = K == 1 ? 2 : 1;  // v_pk_fma_f32 works on a pair of f32 registers
 	T a[kChains][kLanes];
 #pragma unroll
@@ -850,13 +921,11 @@ __global__ void __launch_bounds__(256) k_valu_peak(int iters, float seed, float*
 		for (int u = 0; u < 4; u++)
 #pragma unroll
 			for (int k = 0; k < kChains; k++) {
-				if constexpr (K == 0) {
-					asm volatile("v_fma_f32 %0, %0, 0.5, 1.0" : "+v"(a[k][0]));
-				} else if constexpr (K == 1) {
+				if constexpr (K == 1) {
 					asm volatile("v_pk_fma_f32 %0, %0, 0.5, 1.0 op_sel_hi:[1,0,0]"
 					             : "+v"(*reinterpret_cast<HIP_vector_base<float, 2>::Native_vec_*>(&a[k][0])));
 				} else {
-					asm volatile("v_fma_f64 %0, %0, 0.5, 1.0" : "+v"(a[k][0]));
+					valu_op<K>(a[k][0]);
 				}
 			}
 	}
@@ -998,10 +1067,37 @@ hipError_t launch_stream_read(const void* buf, int64_t bytes, int width, unsigne
 hipError_t launch_valu_peak(int iters, int kind, int waves_per_simd, void* sink, hipStream_t stream) {
 	const unsigned grid = 256 * std::max(1, waves_per_simd);  // blocks of 4 waves (one per SIMD) on every CU
 	float* out = static_cast<float*>(sink);
+	if (kind < 0 || kind >= kValuKinds) return hipErrorInvalidValue;
+	auto go = [&](auto k) {
+		hipLaunchKernelGGL(k_valu_peak<decltype(k)::value>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, out);
+	};
 	switch (kind) {
-		case 0: hipLaunchKernelGGL(k_valu_peak<0>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, out); break;
-		case 1: hipLaunchKernelGGL(k_valu_peak<1>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, out); break;
-		default: hipLaunchKernelGGL(k_valu_peak<2>, dim3(grid), dim3(256), 0, stream, iters, 1.0f, out); break;
+		case 0: go(std::integral_constant<int, 0>{}); break;
+		case 1: go(std::integral_constant<int, 1>{}); break;
+		case 2: go(std::integral_constant<int, 2>{}); break;
+		case 3: go(std::integral_constant<int, 3>{}); break;
+		case 4: go(std::integral_constant<int, 4>{}); break;
+		case 5: go(std::integral_constant<int, 5>{}); break;
+		case 6: go(std::integral_constant<int, 6>{}); break;
+		case 7: go(std::integral_constant<int, 7>{}); break;
+		case 8: go(std::integral_constant<int, 8>{}); break;
+		case 9: go(std::integral_constant<int, 9>{}); break;
+		case 10: go(std::integral_constant<int, 10>{}); break;
+		case 11: go(std::integral_constant<int, 11>{}); break;
+		case 12: go(std::integral_constant<int, 12>{}); break;
+		case 13: go(std::integral_constant<int, 13>{}); break;
+		case 14: go(std::integral_constant<int, 14>{}); break;
+		case 15: go(std::integral_constant<int, 15>{}); break;
+		case 16: go(std::integral_constant<int, 16>{}); break;
+		case 17: go(std::integral_constant<int, 17>{}); break;
+		case 18: go(std::integral_constant<int, 18>{}); break;
+		case 19: go(std::integral_constant<int, 19>{}); break;
+		case 20: go(std::integral_constant<int, 20>{}); break;
+		case 21: go(std::integral_constant<int, 21>{}); break;
+		case 22: go(std::integral_constant<int, 22>{}); break;
+		case 23: go(std::integral_constant<int, 23>{}); break;
+		case 24: go(std::integral_constant<int, 24>{}); break;
+		default: go(std::integral_constant<int, 25>{}); break;
 	}
 	return hipGetLastError();
 }
