@@ -311,16 +311,26 @@ def solo_pass(scene_path, W, H, kw, frames, device):
     ptrs = ([o.data_ptr() for o in outs], [o.data_ptr() for o in out8s])
     s.render_batch_device(prm, *ptrs, stream)  # allocations
     acc = {"ms": [0.0] * 3, "launches": [0] * 3, "bytes": [0] * 3, "flops": [0] * 3, "wall": 0.0}
+    # the work counts: the same call with the counting kernels (rt_render_params.work_stats;
+    # counting costs ~6% of the traversal kernels' time, so the timed call runs without it)
+    counted = s.render_batch_device([s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1, work_stats=True)]
+                                    * frames, *ptrs, stream)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     st = s.render_batch_device(prm, *ptrs, stream)
     acc["wall"] += time.perf_counter() - t0
-    nb, fl = stage_work(st)
+    nb, fl = stage_work(counted)
     for k in range(3):
         acc["ms"][k] += st.stage_ms[k]
         acc["launches"][k] += st.stage_launches[k]
         acc["bytes"][k] += nb[k]
         acc["flops"][k] += fl[k]
+    per = lambda xs: [x // frames for x in xs]
+    acc["work_per_frame"] = {"node_visits": per(counted.stage_node_visits), "tri_tests": per(counted.stage_tri_tests),
+                             "candidates": per(counted.stage_candidates),
+                             "sphere_tests": per(counted.stage_sphere_tests),
+                             "bvh_traversals": per(counted.stage_bvh_traversals),
+                             "max_node_visits_per_ray": list(counted.stage_max_node_visits)}
     s.close()
     return acc
 
@@ -583,8 +593,7 @@ def main():
     n_frames_rank0 = B if partition else B * world
     frames = torch.empty((n_frames_rank0, H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
 
-    totals = {"rays": 0, "trace_rays": 0, "zero": 0, "ms": [0.0] * 3, "launches": [0] * 3, "bytes": [0] * 3,
-              "flops": [0] * 3}
+    totals = {"rays": 0, "trace_rays": 0, "zero": 0, "ms": [0.0] * 3, "launches": [0] * 3}
     work = {}
     n_steps = [0]
 
@@ -616,19 +625,13 @@ def main():
             totals["rays"] += st.trace_rays + st.shadow_rays
             totals["trace_rays"] += st.trace_rays
             totals["zero"] += st.shadow_rays_zero_terms
-            nb, fl = stage_work(st)
             for j in range(3):
                 totals["ms"][j] += st.stage_ms[j]
                 totals["launches"][j] += st.stage_launches[j]
-                totals["bytes"][j] += nb[j]
-                totals["flops"][j] += fl[j]
-            per = lambda xs: [x // B for x in xs]  # the batch's B renders do identical work
+            # the batch's B renders do identical work; the traversal counts (node visits ...)
+            # come from the solo pass's counting call (the timed kernels do not count)
             work.update({"trace_rays": st.trace_rays // B, "shadow_rays": st.shadow_rays // B,
-                         "shadow_rays_zero_terms": st.shadow_rays_zero_terms // B,
-                         "node_visits": per(st.stage_node_visits), "tri_tests": per(st.stage_tri_tests),
-                         "candidates": per(st.stage_candidates), "sphere_tests": per(st.stage_sphere_tests),
-                         "bvh_traversals": per(st.stage_bvh_traversals),
-                         "max_node_visits_per_ray": list(st.stage_max_node_visits)})
+                         "shadow_rays_zero_terms": st.shadow_rays_zero_terms // B})
 
     for _ in range(a.warmup):
         step(False)
@@ -662,8 +665,7 @@ def main():
         lat.append(time.perf_counter() - t1)
     lat = sorted(lat)[len(lat) // 2] if lat else float("nan")
     vals = [elapsed, float(totals["rays"]), float(totals["trace_rays"]), lat, float(totals["zero"]), t_rank] + \
-        totals["ms"] + [float(x) for x in totals["launches"]] + [float(x) for x in totals["bytes"]] + \
-        [float(x) for x in totals["flops"]]
+        totals["ms"] + [float(x) for x in totals["launches"]]
     agg = torch.tensor(vals, dtype=torch.float64, device="cuda")
     if world > 1:
         allv = [torch.empty_like(agg) for _ in range(world)]
@@ -729,6 +731,7 @@ def main():
             "roofline": roofline(solo, a.solo_frames, traffic_path, concurrent, latest_valu()) if solo else None,
             "parity": parity,
             "work_per_frame_rank0": work,
+            "traversal_work_per_frame": solo["work_per_frame"] if solo else None,
             "strong_scaling": sweep,
         }
         if res["roofline"]:

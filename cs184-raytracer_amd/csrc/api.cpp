@@ -105,11 +105,13 @@ struct PlanKey {
 	int32_t width, height, depth, io;
 	int32_t direct_levels;  // the schedule's split of direct and batched shading (a graph bakes it in)
 	int32_t deep_split;     // levels shaded alone after the chain (per call: single frame or batch)
+	int32_t work_stats;     // the traversal kernels' counting instantiation (a graph bakes it in)
 	int64_t n0;
 	uint64_t rows_hash;  // the chunk's image rows (they decide the level counts)
 	bool operator==(const PlanKey& o) const {
 		return width == o.width && height == o.height && depth == o.depth && io == o.io &&
-		       direct_levels == o.direct_levels && deep_split == o.deep_split && n0 == o.n0 &&
+		       direct_levels == o.direct_levels && deep_split == o.deep_split && work_stats == o.work_stats &&
+		       n0 == o.n0 &&
 		       rows_hash == o.rows_hash;
 	}
 };
@@ -222,6 +224,7 @@ struct rt_scene {
 	// chunk shape host-driven itself
 	std::vector<Plan> shared_plans;
 	int plan_share = 1;                          // RTAMD_PLAN_SHARE
+	bool force_work_stats = false;               // RTAMD_WORK_STATS: every call counts (rt_render_params::work_stats)
 	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
 	int shadow_all_lights = 3;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
 	// RTAMD_LIGHT_MAJOR_BELOW: a shading launch with fewer hits than this traces light-major
@@ -472,6 +475,7 @@ struct Render {
 		k.io = ln.io;
 		k.direct_levels = direct_levels;
 		k.deep_split = deep_split;
+		k.work_stats = s->ds.work_stats;
 		k.n0 = ln.n0;
 		k.rows_hash = ln.rows_hash;
 		return k;
@@ -1144,6 +1148,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_may_raise = fs.n_may_raise;
 	s->ds.treelet_root = fs.treelet_root;
+	if (const char* ws = std::getenv("RTAMD_WORK_STATS")) s->force_work_stats = std::atoi(ws) != 0;
 	s->ds.treelet_count = std::min(fs.treelet_count, rtamd::kTreeletNodes);
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	// j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
@@ -1586,6 +1591,9 @@ int render_batch(rt_scene* s, int n, const rt_render_params* params, double* con
 	}
 	HIP_TRY(hipSetDevice(s->device));
 	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
+	// the traversal kernels' instantiation: with the work counters only when asked for
+	s->ds.work_stats = s->force_work_stats;
+	for (int k = 0; k < n; k++) s->ds.work_stats = s->ds.work_stats || params[k].work_stats != 0;
 	rt_counters total{};
 	total.intersection_max = 2.2250738585072014e-308;
 	std::vector<Job> jobs;

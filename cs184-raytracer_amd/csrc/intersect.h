@@ -202,33 +202,53 @@ __device__ bool hits_bounding_box(V3 o, V3 d, P mn, P mx) {
 	return false;
 }
 
-// Per-lane work counters (algorithmic bytes/flops of the roofline)
-// (RT_STATS_LDS: the counters live in the block's LDS, one slot per lane, and are bumped
-// with ds_add: five fewer VGPRs in the traversal loops, where every VGPR counts)
+// Per-lane work counters (algorithmic bytes/flops of the roofline), counted
+// only by the kernels instantiated with kCount (rt_render_params::work_stats): counting
+// costs 6% of the traversal kernels' time, so renders that do not ask for
+// the counts run kernels without them (WorkStats<false>: every member a no-op, reads 0).
+// RT_STATS_LDS: the counters live in the block's LDS, one slot per lane, and are bumped
+// with ds_add (five fewer VGPRs in the traversal loops, where every VGPR counts).
 #ifndef RT_STATS_LDS
 #define RT_STATS_LDS 1
 #endif
 enum WorkCounter : int { W_NODES = 0, W_TRIS, W_CANDS, W_SPHERES, W_ENTRIES, W_COUNT };
+template <bool kCount>
 struct WorkStats {
+	static constexpr bool kOn = kCount;
 #if RT_STATS_LDS
 	uint32_t* c;  // this lane's counters: c[k * kBlock]
 	__device__ __forceinline__ void init(uint32_t* lds) {
-		c = lds + threadIdx.x;
+		if constexpr (kCount) {
+			c = lds + threadIdx.x;
 #pragma unroll
-		for (int k = 0; k < W_COUNT; k++) c[k * kBlock] = 0;
+			for (int k = 0; k < W_COUNT; k++) c[k * kBlock] = 0;
+		}
 	}
-	template <int K>
-	__device__ __forceinline__ void inc() { atomicAdd(c + K * kBlock, 1u); }
-	__device__ __forceinline__ uint32_t get(int k) const { return c[k * kBlock]; }
+	__device__ __forceinline__ void inc(int k) {
+		if constexpr (kCount) atomicAdd(c + k * kBlock, 1u);
+	}
+	// counts a lane where b (the packet loops: every lane adds 0 or 1, no exec-mask
+	// save/restore around the LDS atomic)
+	__device__ __forceinline__ void add(int k, bool b) {
+		if constexpr (kCount) atomicAdd(c + k * kBlock, static_cast<uint32_t>(b));
+	}
+	__device__ __forceinline__ uint32_t get(int k) const {
+		if constexpr (kCount) return c[k * kBlock];
+		return 0;
+	}
 #else
 	uint32_t c[W_COUNT];
 	__device__ __forceinline__ void init(uint32_t*) {
 #pragma unroll
 		for (int k = 0; k < W_COUNT; k++) c[k] = 0;
 	}
-	template <int K>
-	__device__ __forceinline__ void inc() { c[K]++; }
-	__device__ __forceinline__ uint32_t get(int k) const { return c[k]; }
+	__device__ __forceinline__ void inc(int k) {
+		if constexpr (kCount) c[k]++;
+	}
+	__device__ __forceinline__ void add(int k, bool b) {
+		if constexpr (kCount) c[k] += b;
+	}
+	__device__ __forceinline__ uint32_t get(int k) const { return kCount ? c[k] : 0; }
 #endif
 #if RT_PHASE_PROF
 	uint32_t ph[kPhaseSlots];  // shader-clock cycles per phase while this lane was active
@@ -338,10 +358,10 @@ __device__ __forceinline__ bool face_facing_rejects(FP F, V3 d, bool reverse) {
 // strictly closer, or equally close with a smaller reference index: over any visiting
 // order this selects the same face as the reference's in-order scan.
 // Returns true when kAnyHit and the face passes (the caller's question is answered).
-template <bool kAnyHit, bool kUniform = false>
+template <bool kAnyHit, bool kUniform = false, typename WS>
 __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn, bool reverse,
-                                          double any_limit, MeshBest& best, WorkStats& ws) {
-	ws.inc<W_TRIS>();
+                                          double any_limit, MeshBest& best, WS& ws) {
+	ws.inc(W_TRIS);
 	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
 	// A wave-uniform record (RT_FACE_ONE_FETCH): vertices, id and cone in one round of scalar
 	// loads before the facing pre-test, else the vertices wait for a second memory round
@@ -389,7 +409,7 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	if (t < 0) return false;
 	const double dist = t * dn;
 	if (!(dist < best.dist || (dist == best.dist && id < best.id))) return false;
-	ws.inc<W_CANDS>();
+	ws.inc(W_CANDS);
 	const V3 tn = face_normal<kUniform>(S, f, a, b);
 	const bool front = dot4z(tn, d) < 0;
 	if (!front ^ reverse) return false;
@@ -418,11 +438,11 @@ __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 // kUniform false (RT_PRED_FACE_LANE): the per-lane LBVH search's form, each lane on a face
 // of its own leaf (f must index a face for every lane, `on` or not); the vertices are
 // fetched after the facing pre-test, as in test_face.
-template <bool kAnyHit, bool kUniform = true>
+template <bool kAnyHit, bool kUniform = true, typename WS>
 __device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn,
-                                               bool reverse, double any_limit, MeshBest& best, WorkStats& ws,
+                                               bool reverse, double any_limit, MeshBest& best, WS& ws,
                                                bool on) {
-	if (on) ws.inc<W_TRIS>();
+	ws.add(W_TRIS, on);
 	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
 	V3 p0, va, vb;
 	int32_t id;
@@ -461,7 +481,7 @@ __device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, 
 	const double dist = t * dn;
 	ok = ok && t >= 0 && (dist < best.dist || (dist == best.dist && id < best.id));
 	if (!wave_any(ok)) return false;
-	if (ok) ws.inc<W_CANDS>();
+	ws.add(W_CANDS, ok);
 	const V3 tn = face_normal<kUniform>(S, f, a, b);
 	const bool front = dot4z(tn, d) < 0;
 	ok = ok && !(!front ^ reverse);
@@ -698,10 +718,10 @@ __device__ __forceinline__ bool world_slab32(GP G, const WorldRay32& r, float li
 //   prune_cap are skipped (faces there cannot decide it either).  Otherwise completes
 //   like the closest-hit search restricted to dist <= prune_cap.
 // The search itself, without the reference's bounding-box gate (see mesh_hit).
-template <bool kAnyHit, typename GP>
+template <bool kAnyHit, typename GP, typename WS>
 __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
                          double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
-                         DeviceCounters* ctr, WorkStats& ws) {
+                         DeviceCounters* ctr, WS& ws) {
 	settled = false;
 	const double dn = sqrt(d.x * d.x + (d.y * d.y + d.z * d.z));  // Vector3d::norm
 	const V3 nd = -d;
@@ -724,7 +744,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		// node and face work do not interleave within a wave.  `ref` >= 0 is a node,
 		// <= -2 a leaf (face offset << 3 | count), -1 done.  The far child of a node whose
 		// two children are hit is pushed (LDS stack, kStackDepth entries per lane).
-		ws.inc<W_ENTRIES>();
+		ws.inc(W_ENTRIES);
 #if RT_DIAG_LANES
 		diag_lanes(kAnyHit ? 24 : 8, true);  // wave slots and lanes entering a per-lane LBVH search
 #endif
@@ -743,7 +763,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		while (ref != -1 || leaf != -1) {
 			PROF_BEGIN(tn);
 			while (ref >= 0) {
-				ws.inc<W_NODES>();
+				ws.inc(W_NODES);
 				// the child references are read with the boxes (one memory round trip per node)
 				NodeRec nr;
 				fetch_node(S, ref, nr);
@@ -840,10 +860,10 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 // The reference tests a gated mesh only when hitsBoundingBox passes (geometry.cpp:72); the
 // search has no side effects, so the gate (six divisions) is evaluated only for rays the
 // search reports a hit (or occluder) for: the same outcome for fewer rays.
-template <bool kAnyHit, typename GP>
+template <bool kAnyHit, typename GP, typename WS>
 __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
 double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
-DeviceCounters* ctr, WorkStats& ws) {
+DeviceCounters* ctr, WS& ws) {
 if (!mesh_search<kAnyHit>(S, G, o, d, reverse, any_limit, prune_cap, fh, settled, found_dist, stack, ctr, ws))
 return false;
 PROF_BEGIN(tg);
@@ -913,8 +933,9 @@ __device__ __forceinline__ void check_may_raise(const DeviceScene& S, V3 d, bool
 // insertion order.  A geometry whose padded world box the ray misses, or enters beyond
 // the current best distance, cannot be the answer and is skipped without its
 // object-space transform.
+template <typename WS>
 __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, double& best_dist, int& best_geom, V3& hitP,
-                            V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WorkStats& ws) {
+                            V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WS& ws) {
 	bool found = false;
 	FaceHit best{-1, 0, 0};
 #if RT_WORLD32
@@ -942,7 +963,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
-			ws.inc<W_SPHERES>();
+			ws.inc(W_SPHERES);
 			PROF_BEGIN(ts);
 			hit = sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
@@ -969,9 +990,9 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 // face up to slightly beyond it means no occlusion.  Only a closest face within a
 // relative 1e-7 of the light distance falls back to the reference's full comparison.
 // geom_occludes: geometry G (its world box already passed) occludes the shadow ray.
-template <typename GP>
+template <typename GP, typename WS>
 __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double dist_light,
-                              int32_t* stack, DeviceCounters* ctr, WorkStats& ws) {
+                              int32_t* stack, DeviceCounters* ctr, WS& ws) {
 	const bool inf_light = dist_light == INFINITY;
 	PROF_BEGIN(tx);
 	const V3 oo = xf_point(G->inv, o);
@@ -984,7 +1005,7 @@ __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool rever
 	bool hit, settled = false;
 	double fd;
 	if (G->kind == DGEOM_SPHERE) {
-		ws.inc<W_SPHERES>();
+		ws.inc(W_SPHERES);
 		PROF_BEGIN(ts);
 		hit = sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
@@ -1014,8 +1035,9 @@ __device__ __forceinline__ double shadow_slab_limit(double dist_light) {
 }
 
 // The `any` over the geometries, cheap ones first (DeviceScene::shadow_order).
+template <typename WS>
 __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, int32_t* stack,
-                         DeviceCounters* ctr, WorkStats& ws) {
+                         DeviceCounters* ctr, WS& ws) {
 #if RT_WORLD32
 	const WorldRay32 wr = world_ray32(o, d);
 	const float lim = world_lim32(shadow_slab_limit(dist_light));
@@ -1054,10 +1076,10 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 // that index are fetched with scalar loads instead of 64 identical vector loads.
 __device__ __forceinline__ int32_t uniform_i32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-template <bool kAnyHit, typename GP>
+template <bool kAnyHit, typename GP, typename WS>
 __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, bool on, double any_limit,
                                 double prune_cap, FaceHit& fh, bool& settled, double& found_dist,
-                                int32_t* wstack, WorkStats& ws) {
+                                int32_t* wstack, WS& ws) {
 	settled = false;
 	const double dn = sqrt(d.x * d.x + (d.y * d.y + d.z * d.z));  // Vector3d::norm
 	const V3 nd = -d;
@@ -1080,7 +1102,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			}
 				PROF_END(ws, PH_FACES, tf);
 		} else if (!(RT_DIAG_SKIP & 1)) {
-			if (live) ws.inc<W_ENTRIES>();
+			ws.add(W_ENTRIES, live);
 			const V3 inv = safe_inv(d);
 			const Ray32 r32 = ray32(G, o, d, inv);
 			float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);  // changes only with best.dist
@@ -1108,7 +1130,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			// ballot, no instruction)
 			for (;;) {
 				PROF_BEGIN(tn);
-				if (live) ws.inc<W_NODES>();
+				ws.add(W_NODES, live);
 				float tn0 = 0, tn1 = 0;
 				const bool s0 = slab32(box[0][0], box[0][1], r32, lim, tn0);
 				const bool s1 = slab32(box[1][0], box[1][1], r32, lim, tn1);
@@ -1180,9 +1202,10 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	return true;
 }
 
+template <typename WS>
 __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, bool on, double& best_dist,
                                    int& best_geom, V3& hitP, V3& hitNobj, int32_t* wstack, DeviceCounters* ctr,
-                                   WorkStats& ws) {
+                                   WS& ws) {
 	bool found = false;
 	FaceHit best{-1, 0, 0};
 #if RT_WORLD32
@@ -1211,7 +1234,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 		bool hit, settled;
 		double fd;
 		if (G->kind == DGEOM_SPHERE) {
-			if (cand) ws.inc<W_SPHERES>();
+			ws.add(W_SPHERES, cand);
 			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
@@ -1234,8 +1257,9 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 }
 
 // Packet form of occluded(): same decisions per lane (see occluded()).
+template <typename WS>
 __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, bool on,
-                                int32_t* wstack, DeviceCounters* ctr, WorkStats& ws) {
+                                int32_t* wstack, DeviceCounters* ctr, WS& ws) {
 	const bool inf_light = dist_light == INFINITY;
 #if RT_WORLD32
 	const WorldRay32 wr = world_ray32(o, d);
@@ -1271,7 +1295,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		bool hit, settled = false;
 		double fd = INFINITY;
 		if (G->kind == DGEOM_SPHERE) {
-			if (cand) ws.inc<W_SPHERES>();
+			ws.add(W_SPHERES, cand);
 			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);

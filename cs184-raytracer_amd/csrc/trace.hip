@@ -129,7 +129,8 @@ __device__ __forceinline__ unsigned long long* shard(unsigned long long* stats) 
 
 
 
-__device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long long* stats, int stage, int packet = 0) {
+template <typename WS>
+__device__ __forceinline__ void flush_stats(const WS& ws, unsigned long long* stats, int stage, int packet = 0) {
 #if RT_PHASE_PROF
 #pragma unroll
 	for (int k = 0; k < kPhaseSlots; k++) {
@@ -138,6 +139,7 @@ __device__ __forceinline__ void flush_stats(const WorkStats& ws, unsigned long l
 		if (__lane_id() == 0 && v) atomicAdd(&g_phase[(stage * 2 + packet) * kPhaseSlots + k], v);
 	}
 #endif
+	if constexpr (!WS::kOn) return;
 	unsigned long long w[5] = {ws.get(W_NODES), ws.get(W_TRIS), ws.get(W_CANDS), ws.get(W_SPHERES), ws.get(W_ENTRIES)};
 	unsigned long long wmax = w[0];
 #pragma unroll
@@ -198,7 +200,7 @@ __device__ __forceinline__ Slots block_append2(bool a, bool b0, bool b1, int32_t
 // shading, so they are spawned here and level L+1 can be traced while level L is shaded.
 // One item (thread t of the level's index space) of k_closest; every thread of the block
 // calls it (block_append2 synchronises the block).
-template <bool kPacket>
+template <bool kPacket, bool kCount>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
                                              int remaining, int plan_last, const RayLevel* levels,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
@@ -208,7 +210,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	const int next_level = remaining > 0 ? level + 1 : level;
 	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
-	WorkStats ws{};
+	WorkStats<kCount> ws{};
 	ws.init(stat_lds);
 	PROF_BEGIN(t_total);
 	bool hit = false;
@@ -344,7 +346,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 // before the host knows their size: the ray count is read from the previous level's
 // child counter (n_dev) and a fixed grid strides over it, so each level is queued behind
 // the previous one without a host round trip.
-template <bool kPacket>
+template <bool kPacket, bool kCount>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
                                                                       int64_t n_host, const int32_t* n_dev,
@@ -352,7 +354,7 @@ __global__ void __launch_bounds__(kBlock)
                                                                       const RayLevel* levels, DeviceCounters* ctr,
                                                                       unsigned long long* stats) {
 	__shared__ AppendLds append_lds;
-	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
+	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
 	if constexpr (!kPacket) load_treelet(S);
@@ -370,7 +372,7 @@ __global__ void __launch_bounds__(kBlock)
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
-		closest_item<kPacket>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
+		closest_item<kPacket, kCount>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
 		                      append_lds, stack, stat_lds);
 	}
 }
@@ -500,7 +502,7 @@ struct HitStage {
 	}
 };
 
-template <bool kPacket>
+template <bool kPacket, bool kCount>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
                                             uint32_t* stat_lds, double* hit_lds) {
@@ -509,7 +511,7 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	const BatchItem it = batch_item<true>(B, nl, tg);
 	const int level = it.level;
 	const int64_t t = it.local, nh = it.nh;
-	WorkStats ws{};
+	WorkStats<kCount> ws{};
 	ws.init(stat_lds);
 	PROF_BEGIN(t_total);
 	int j0 = 0, j1 = nl;
@@ -626,20 +628,20 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 
 // Host-counted batches launch one thread per item; device-counted ones a fixed grid that
 // strides over the items (the bound is block-uniform: no lane of a wave leaves early).
-template <bool kPacket>
+template <bool kPacket, bool kCount>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
-	__shared__ uint32_t stat_lds[W_COUNT * kBlock];
+	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
 	__shared__ double hit_lds[(kPacket && RT_HIT_LDS) ? 9 * kBlock : 1];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
 	if constexpr (!kPacket) load_treelet(S);
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
-		shadow_item<kPacket>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds, hit_lds);
+		shadow_item<kPacket, kCount>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds, hit_lds);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -966,12 +968,15 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 	// with a device-side count, n is an upper bound: a grid of at most kStrideBlocks
 	const unsigned grid = n_dev ? (unsigned)std::min<int64_t>(grid_for(threads, kBlock), kStrideBlocks)
 	                            : grid_for(threads, kBlock);
-	if (packet)
-		hipLaunchKernelGGL(k_closest<true>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
+	// the counting kernels only for renders that asked for the work counts (work_stats)
+	auto go = [&](auto kernel) {
+		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
 		                   plan_last, levels_dev, ctr, stats);
+	};
+	if (packet)
+		s.work_stats ? go(k_closest<true, true>) : go(k_closest<true, false>);
 	else
-		hipLaunchKernelGGL(k_closest<false>, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev,
-		                   remaining_depth, plan_last, levels_dev, ctr, stats);
+		s.work_stats ? go(k_closest<false, true>) : go(k_closest<false, false>);
 	return hipGetLastError();
 }
 
@@ -996,10 +1001,13 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 	const int64_t items = b.shadow_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0 || s.n_nonambient <= 0) return hipSuccess;
 	const unsigned grid = b.dev_counts ? dev_grid(items, kBlock) : grid_for(items, kBlock);
+	auto go = [&](auto kernel) {
+		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
+	};
 	if (shadow_packet(b, packet_mask))
-		hipLaunchKernelGGL(k_shadow<true>, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
+		s.work_stats ? go(k_shadow<true, true>) : go(k_shadow<true, false>);
 	else
-		hipLaunchKernelGGL(k_shadow<false>, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
+		s.work_stats ? go(k_shadow<false, true>) : go(k_shadow<false, false>);
 	return hipGetLastError();
 }
 

@@ -56,7 +56,7 @@ class rt_render_params(ctypes.Structure):
     _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("bounce_depth", ctypes.c_int32),
                 ("intersection_only", ctypes.c_int32), ("row_begin", ctypes.c_int32), ("row_end", ctypes.c_int32),
                 ("row_step", ctypes.c_int32), ("chunk_pixels", ctypes.c_int32), ("row_block", ctypes.c_int32),
-                ("reserved", ctypes.c_int32)]
+                ("work_stats", ctypes.c_int32)]
 
 
 class rt_counters(ctypes.Structure):
@@ -317,9 +317,11 @@ class Scene:
 
     def params(self, width: int, height: int, bounce_depth: int, intersection_only: bool, row_begin: int = 0,
                row_end: Optional[int] = None, row_step: int = 1, chunk_pixels: int = 0,
-               row_block: int = 1) -> rt_render_params:
+               row_block: int = 1, work_stats: bool = False) -> rt_render_params:
+        """``work_stats``: count the traversal work (RenderStats.node_visits ...; rt_render_params)."""
         return rt_render_params(width, height, bounce_depth, int(bool(intersection_only)), row_begin,
-                                height if row_end is None else row_end, row_step, chunk_pixels, row_block, 0)
+                                height if row_end is None else row_end, row_step, chunk_pixels, row_block,
+                                int(bool(work_stats)))
 
     def renderScene(self, output: Optional[np.ndarray] = None,
                     phandler: Optional[Callable[[int, int], None]] = None, options: Optional[Options] = None,

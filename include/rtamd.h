@@ -168,7 +168,12 @@ typedef struct rt_render_params {
 	/* Pixels per wavefront pass (bounds queue memory); 0 = automatic. */
 	int32_t chunk_pixels;
 	int32_t row_block;            /* see row_begin; 0 = 1 */
-	int32_t reserved;
+	/* Nonzero: count the traversal work into rt_counters (node_visits, tri_tests, candidates,
+	 * sphere_tests and their stage_* splits) with the counting instantiation of the
+	 * traversal kernels, about 6% slower; 0 (the default): those counters read 0.  Images
+	 * are bitwise equal either way.  Any nonzero entry of a batch counts the whole call;
+	 * RTAMD_WORK_STATS=1 in the environment counts every call. */
+	int32_t work_stats;
 } rt_render_params;
 
 typedef struct rt_counters {

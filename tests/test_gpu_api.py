@@ -283,3 +283,38 @@ def test_multi_frame_chunks(gpu, oracle, pack, graph, monkeypatch):
         single[1] += one.shadow_rays
     assert [st.trace_rays, st.shadow_rays] == single
     s.close()
+
+
+@pytest.mark.parametrize("graph", ["2", "1"])
+def test_work_counters_are_optional(gpu, monkeypatch, graph):
+    """rt_render_params.work_stats selects the counting instantiation of the traversal
+    kernels: the same bits either way, the traversal counters nonzero only when asked for
+    (RTAMD_WORK_STATS=1 asks for every call); plans and graphs keyed on it."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("RTAMD_GRAPH", graph)
+    w, h = 96, 64
+    s = gpu.load_scene(os.path.join(SCENES, "excess_inputs/bunny.rti"))
+    outs = {}
+    for rep in range(2):  # the second round replays the plans of the first
+        for count in (False, True):
+            out = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda")
+            st = s.render_device(s.params(w, h, 4, False, work_stats=count), out.data_ptr(), 0)
+            torch.cuda.synchronize()
+            outs[(rep, count)] = out.cpu().numpy()
+            counters = (st.node_visits, st.tri_tests, st.candidates, st.sphere_tests) + tuple(st.stage_node_visits) + \
+                tuple(st.stage_bvh_traversals)
+            assert st.trace_rays > 0 and st.shadow_rays > 0
+            if count:
+                assert st.node_visits > 0 and st.tri_tests > 0 and st.sphere_tests > 0
+            else:
+                assert not any(counters), counters
+    ref = outs[(0, False)]
+    assert all(np.array_equal(ref.view(np.uint64), o.view(np.uint64)) for o in outs.values())
+    s.close()
+    monkeypatch.setenv("RTAMD_WORK_STATS", "1")
+    s = gpu.load_scene(os.path.join(SCENES, "excess_inputs/bunny.rti"))
+    out = torch.zeros((h, w, 3), dtype=torch.float64, device="cuda")
+    st = s.render_device(s.params(w, h, 4, False), out.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert st.node_visits > 0 and np.array_equal(out.cpu().numpy().view(np.uint64), ref.view(np.uint64))
+    s.close()

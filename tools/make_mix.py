@@ -13,10 +13,10 @@ def load(d):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     launches = collections.defaultdict(set)
     for r in csv.DictReader(open(os.path.join(d, f))):
-        m = re.search(r"k_\w+(<\w+>)?", r["Kernel_Name"])
-        if not m:
+        m = re.search(r"k_\w+(<[\w, ]+>)?", r["Kernel_Name"])
+        if not m or m.group(0).endswith(", true>"):  # counting instantiations (bench.py solo pass)
             continue
-        k = m.group(0)
+        k = m.group(0).replace(", false>", ">")
         per[k][r["Counter_Name"]] += float(r["Counter_Value"])
         launches[k].add(r["Dispatch_Id"])
     return per, {k: len(v) for k, v in launches.items()}

@@ -24,8 +24,12 @@ CALIB_BYTES = 1 << 30
 
 
 def family(name):
-    m = re.search(r"(k_[a-z0-9_]+)(?:<[^>]*>)?\(", name)
-    return m.group(1) if m else None
+    """Kernel family; None for the counting instantiations (<..., true>: bench.py's solo pass
+    makes one counting call for the work counts, the roofline times the other)."""
+    m = re.search(r"(k_[a-z0-9_]+)(<[^>]*>)?\(", name)
+    if not m or (m.group(2) and m.group(2).endswith(", true>")):
+        return None
+    return m.group(1)
 
 
 def per_dispatch(path, counter):

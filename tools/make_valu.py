@@ -28,8 +28,12 @@ N_XCD, N_CU, N_SIMD = 8, 256, 1024
 
 
 def variant(name):
+    """k_shadow<true> etc.; None for the counting instantiations (<..., true>: bench.py's solo
+    pass makes one counting call for the work counts, the roofline times the other)."""
     m = re.search(r"(k_[a-z0-9_]+(?:<[^>]*>)?)\(", name)
-    return m.group(1).replace("(anonymous namespace)::", "") if m else None
+    if not m or m.group(1).endswith(", true>"):
+        return None
+    return m.group(1).replace("(anonymous namespace)::", "").replace(", false>", ">")
 
 
 def family(v):
