@@ -75,7 +75,7 @@ def main():
     fetch = per_dispatch(f"{src}/fetch/pmc_counter_collection.csv", "FETCH_SIZE")
     write = per_dispatch(f"{src}/write/pmc_counter_collection.csv", "WRITE_SIZE")
     out = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over `bench.py "
-                     "--solo-only --solo-frames 3` (every kernel alone); per kernel family, mean per launch; "
+                     "--solo-only --solo-frames 4` (every kernel alone); per kernel family, mean per launch; "
                      f"FETCH_SIZE x {factor} (measured: tools/fetch_calibration.py, 1 GiB read at 1/4/8/16 B per "
                      "lane), WRITE_SIZE as counted (exact for streaming stores, MI355X_MICROARCH.md); kB x 1024",
            "fetch_calibration": cal, "fetch_factor": factor, "fetch_factors_seen": factors,
