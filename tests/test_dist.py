@@ -4,7 +4,7 @@ The per-rank renderer here is the CPU oracle (test infrastructure); on GPUs the 
 rtamd.dist code runs with the "nccl" (RCCL) backend and the HIP renderer (bench.py).
 """
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -15,19 +15,16 @@ from cases import SCENES
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A rendezvous for init_process_group: a fresh FileStore path (no TCP port to race for
+    with the other test workers)."""
+    return os.path.join(tempfile.mkdtemp(prefix="rtamd_pg_"), "store")
 
 
 def _worker(rank, world, port, scene, w, h, bdepth, io, q, block=1):
     import torch.distributed as dist
     import pyoracle
     from rtamd import dist as rd
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         def render_rows(rows):
             begin, end, step, block = rows
@@ -71,8 +68,7 @@ def _batch_worker(rank, world, port, scene, w, h, bdepth, q):
     import torch.distributed as dist
     import pyoracle
     from rtamd import dist as rd
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         img, _ = pyoracle.render(scene, w, h, bdepth=bdepth, threads=2)
         full = torch.from_numpy(img)
@@ -108,8 +104,7 @@ def _batch_rows_worker(rank, world, port, scene, w, h, bdepth, block, q):
     import torch.distributed as dist
     import pyoracle
     from rtamd import dist as rd
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         full, _ = pyoracle.render(scene, w, h, bdepth=bdepth, threads=2)
         rows = rd.rows_of(h, rank, world, block)

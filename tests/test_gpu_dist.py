@@ -8,7 +8,7 @@ compared with the unmodified reference's goldens (sha256 of the f64 image).
 """
 import hashlib
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -19,11 +19,9 @@ pytestmark = pytest.mark.gpu
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A rendezvous for init_process_group: a fresh FileStore path (no TCP port to race for
+    with the other test workers)."""
+    return os.path.join(tempfile.mkdtemp(prefix="rtamd_pg_"), "store")
 
 
 def _worker(rank, world, port, scene, w, h, bdepth, io, q, block):
@@ -31,8 +29,8 @@ def _worker(rank, world, port, scene, w, h, bdepth, io, q, block):
     import torch.distributed as dist
     import rtamd
     from rtamd import dist as rd
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
         s = rtamd.load_scene(scene)
