@@ -4,7 +4,8 @@
 Workload (BASELINE.json configs[2], the metric's 1920x1080 single-GPU config):
 excess_inputs/bunny.rti (4,968-triangle bunny + reflective floor +
 mirror spheres), 1920x1080, --bdepth 4.  A step renders a fixed batch of frames
-(--frames-per-step, default 32) of that scene through the C-ABI (librtamd.so); rays =
+(--frames-per-step, default 48: 24 two-frame chunks, 8 on each of the library's 3 batch
+lanes, so that no lane traces a last chunk alone) of that scene through the C-ABI (librtamd.so); rays =
 traceRay calls (primary + reflection + refraction) + shadow rays, counted by the kernels
 and equal to the reference's counts.  Inputs (the scene) are resident in HBM before the
 timed region; every frame is written as the reference's f64 RasterImage and as RGB8.
@@ -68,7 +69,7 @@ def parse():
     ap.add_argument("--row-block", type=int, default=8,
                     help="partition granularity: blocks of this many rows interleaved over the ranks (8 = the "
                          "8x8 ray tiles stay whole)")
-    ap.add_argument("--frames-per-step", type=int, default=32,
+    ap.add_argument("--frames-per-step", type=int, default=48,
                     help="frames per step (partition: in total, every frame split over the ranks; "
                          "replica: per rank)")
     ap.add_argument("--sweep", default="C5_refraction3_4096_bd8,C4_airboat_sub_1920x1080",

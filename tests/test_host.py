@@ -205,11 +205,13 @@ def test_chunk_plan_covers_every_row_once(rt, frames, ways, lanes):
             assert sum(s[3] for s in plan if s[0] == c) == rows
 
 
-def test_chunk_plan_unbalanced_whole_frames(rt):
-    """Whole frames of a 32-frame step keep their two-frame chunks (16 of them: many chunks
-    per lane, so no balancing) and the balancing switch changes nothing there."""
+@pytest.mark.parametrize("frames", [32, 48])
+def test_chunk_plan_unbalanced_whole_frames(rt, frames):
+    """Whole frames of a 32- or 48-frame step (bench.py's default) keep their two-frame chunks
+    (16 or 24 of them: many chunks per lane, so no balancing; 48 frames give every one of the
+    3 lanes 8) and the balancing switch changes nothing there."""
     W, H = 1920, 1080
-    params = [rt.rt_render_params(W, H, 4, 0, 0, H, 1, 0, 1, 0) for _ in range(32)]
+    params = [rt.rt_render_params(W, H, 4, 0, 0, H, 1, 0, 1, 0) for _ in range(frames)]
     a, b = _plan(rt, params, 3, balance=1), _plan(rt, params, 3, balance=0)
     assert a == b
-    assert len({c for c, *_ in a}) == 16 and all(n == H for *_, n in a)
+    assert len({c for c, *_ in a}) == frames // 2 and all(n == H for *_, n in a)
