@@ -14,6 +14,21 @@
 #ifndef RT_SAH_BINS
 #define RT_SAH_BINS 32
 #endif
+// Leaf termination (RT_SAH_LEAF 1): a set of at most RT_LEAF_MAX faces becomes a leaf when
+// its SAH cost n * CI is no more than splitting it, CT + (A_L n_L + A_R n_R) / A * CI;
+// 0: every set of more than kLeafFaces faces is split, smaller ones are leaves.
+#ifndef RT_SAH_LEAF
+#define RT_SAH_LEAF 0
+#endif
+#ifndef RT_LEAF_MAX
+#define RT_LEAF_MAX 7
+#endif
+#ifndef RT_SAH_CT
+#define RT_SAH_CT 1.0
+#endif
+#ifndef RT_SAH_CI
+#define RT_SAH_CI 1.5
+#endif
 
 namespace rtamd {
 namespace {
@@ -94,7 +109,7 @@ struct Builder {
 
 	// Binned surface-area-heuristic split of order[b, e) (reorders it in place): the split
 	// between centroid bins minimising area(L) * |L| + area(R) * |R| over the three axes.
-	int sah_split(int b, int e) {
+	int sah_split(int b, int e, double* cost = nullptr) {
 		constexpr int kBins = RT_SAH_BINS;
 		double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
 		auto centre = [&](int32_t f, int a) { return 0.5 * (boxes[f].lo[a] + boxes[f].hi[a]); };
@@ -141,6 +156,7 @@ struct Builder {
 				}
 			}
 		}
+		if (cost) *cost = best;  // area(L) |L| + area(R) |R| (INFINITY: no split found)
 		if (best_axis < 0) return (b + e) / 2;  // all centroids coincide
 		const double ext = chi[best_axis] - clo[best_axis];
 		auto* mid = std::partition(order.data() + b, order.data() + e, [&](int32_t f) {
@@ -154,7 +170,24 @@ struct Builder {
 		max_depth = std::max(max_depth, depth);
 		Ref r;
 		r.box.empty();
-		if (e - b <= kLeafFaces) {
+		int m = -1;
+		bool leaf = e - b <= kLeafFaces;
+		if (RT_SAH_LEAF && sah && !median_only) {
+			static_assert(RT_LEAF_MAX <= 7, "leaf face counts are 3-bit fields of the traversal's references");
+			leaf = e - b <= 1;
+			if (!leaf) {
+				double split_cost = INFINITY;
+				m = sah_split(b, e, &split_cost);
+				if (e - b <= RT_LEAF_MAX) {
+					Box all;
+					all.empty();
+					for (int i = b; i < e; i++) all.grow(boxes[order[i]]);
+					const double a = area(all);
+					leaf = !(a > 0) || (e - b) * RT_SAH_CI * a <= RT_SAH_CT * a + RT_SAH_CI * split_cost;
+				}
+			}
+		}
+		if (leaf) {
 			r.first = static_cast<int32_t>(leaf_order.size());
 			r.count = e - b;
 			for (int i = b; i < e; i++) {
@@ -165,7 +198,7 @@ struct Builder {
 		}
 		const int idx = static_cast<int>(nodes.size());
 		nodes.emplace_back();
-		const int m = (sah && !median_only) ? sah_split(b, e) : split(b, e);
+		if (m < 0) m = (sah && !median_only) ? sah_split(b, e) : split(b, e);
 		const Ref c[2] = {build(b, m, depth + 1), build(m, e, depth + 1)};
 		DBvhNode& n = nodes[idx];
 		std::memset(&n, 0, sizeof(n));
