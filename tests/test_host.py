@@ -215,3 +215,31 @@ def test_chunk_plan_unbalanced_whole_frames(rt, frames):
     a, b = _plan(rt, params, 3, balance=1), _plan(rt, params, 3, balance=0)
     assert a == b
     assert len({c for c, *_ in a}) == frames // 2 and all(n == H for *_, n in a)
+
+
+def test_ctypes_structs_match_the_header_layout(rt, tmp_path):
+    """The Python mirror's structures (rtamd/__init__.py) have the C header's field offsets
+    and sizes: a C program compiled against include/rtamd.h prints offsetof / sizeof of every
+    field the ctypes classes declare."""
+    import ctypes
+    structs = [getattr(rt, n) for n in dir(rt) if n.startswith("rt_") and isinstance(getattr(rt, n), type)
+               and issubclass(getattr(rt, n), ctypes.Structure)]
+    assert len(structs) >= 10
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "rtamd.h"', "int main(void) {"]
+    want = []
+    for st in structs:
+        name = st.__name__
+        lines.append(f'  printf("%zu\\n", sizeof({name}));')
+        want.append((name, "sizeof", ctypes.sizeof(st)))
+        for f, *_ in st._fields_:
+            lines.append(f'  printf("%zu\\n", offsetof({name}, {f}));')
+            want.append((name, f, getattr(st, f).offset))
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "abi.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "abi"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert len(got) == len(want)
+    bad = [(w, g) for w, g in zip(want, got) if w[2] != g]
+    assert not bad, bad
