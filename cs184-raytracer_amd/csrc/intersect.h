@@ -431,6 +431,11 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 #ifndef RT_PRED_FACE
 #define RT_PRED_FACE 1
 #endif
+// RT_PACKET_TOP: the packet traversal keeps its stack's most recent push in a scalar register,
+// so popping it needs no LDS round trip before the next node's record is requested
+#ifndef RT_PACKET_TOP
+#define RT_PACKET_TOP 0
+#endif
 #ifndef RT_PRED_FACE_LANE
 #define RT_PRED_FACE_LANE 0
 #endif
@@ -1110,6 +1115,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			const int32_t fbase = uniform_i32(G->face_begin);
 			int32_t node = uniform_i32(G->bvh_root);
 			int sp = 0;
+			int32_t top = -1;  // RT_PACKET_TOP: the stack's top entry (-1: none)
 			// the node record: the whole 64 B in one scalar load, both child boxes tested by
 			// every lane (a lane that is done ignores its results)
 			float box[2][2][3];  // [child][lo, hi][axis]
@@ -1150,10 +1156,19 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				int32_t next = -1;
 				if (w_first && c_first == 0) next = f_first;
 				if (w_second && c_second == 0) {
-					if (next < 0)
+					if (next < 0) {
 						next = f_second;
-					else if (sp < kStackDepth)
+					} else if (RT_PACKET_TOP) {
+						// the stack's top entry in a scalar register: pushed below it to LDS
+						if (top >= 0 && sp < kStackDepth) wstack[sp++] = top;
+						top = f_second;
+					} else if (sp < kStackDepth) {
 						wstack[sp++] = f_second;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
+					}
+				}
+				if (RT_PACKET_TOP && next < 0 && top >= 0) {
+					next = top;  // no LDS round trip before the next node's fetch
+					top = -1;
 				}
 				if (next < 0 && sp > 0) next = uniform_i32(wstack[--sp]);
 				if (next >= 0) fetch(next);
