@@ -106,12 +106,13 @@ struct PlanKey {
 	int32_t direct_levels;  // the schedule's split of direct and batched shading (a graph bakes it in)
 	int32_t deep_split;     // levels shaded alone after the chain (per call: single frame or batch)
 	int32_t work_stats;     // the traversal kernels' counting instantiation (a graph bakes it in)
+	int64_t light_major_below;  // shading launches' item layout (per call; a graph bakes it in)
 	int64_t n0;
 	uint64_t rows_hash;  // the chunk's image rows (they decide the level counts)
 	bool operator==(const PlanKey& o) const {
 		return width == o.width && height == o.height && depth == o.depth && io == o.io &&
 		       direct_levels == o.direct_levels && deep_split == o.deep_split && work_stats == o.work_stats &&
-		       n0 == o.n0 &&
+		       light_major_below == o.light_major_below && n0 == o.n0 &&
 		       rows_hash == o.rows_hash;
 	}
 };
@@ -231,11 +232,17 @@ struct rt_scene {
 	// (one lane per (hit, light)) even where the all-lights layout is selected: a few waves per
 	// SIMD each tracing every light in turn leave the GPU latency-bound (one GPU's row share
 	// of a single frame); light-major gives n_lights times the waves, each a shorter chain
-	int64_t light_major_below = 131072;
+	// Per call like direct_levels: a single frame (or one device's row share of it) of a scene
+	// with meshes traces light-major below 1 M hits (C4 0.401 -> 0.354 ms, C2b 0.349 -> 0.326,
+	// C3 1.284 -> 1.259),
+	// a batch below 128 K (its level-1 launch of 2-frame chunks, ~840 K hits, measured -7% as
+	// light-major, and an 8-way row share -3 to -6%: DESIGN.md §4)
+	int64_t light_major_below_single = (int64_t)1 << 20;
+	int64_t light_major_below_batch = (int64_t)1 << 17;
 	// RTAMD_ONE_STREAM_PIXELS: a replayed chunk of at most this many pixels is issued on one
 	// stream (Render::issue_plan)
 	int64_t one_stream_pixels = (int64_t)1 << 17;
-	int all_lights_for(int first_level, int64_t hits) const {
+	int all_lights_for(int first_level, int64_t hits, int64_t light_major_below) const {
 		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
 		if (al && ds.n_nonambient > 1 && hits < light_major_below) al = 0;
 		return al;
@@ -398,6 +405,7 @@ struct Render {
 	rt_scene* s;
 	int direct_levels = 2;  // rt_scene::direct_levels_single or _batch, for this call
 	int deep_split = 0;     // rt_scene::deep_split_single or _batch, for this call
+	int64_t light_major_below = 0;  // rt_scene::light_major_below_single or _batch, for this call
 	rt_counters cnt{};
 	float kernel_ms = 0.f;
 	Progress* progress = nullptr;
@@ -437,7 +445,7 @@ struct Render {
 		b.n = static_cast<int32_t>(lv.size());
 		int64_t hits = 0;
 		for (const auto& l : lv) hits += l.second;
-		b.all_lights = s->all_lights_for(lv.front().first, hits);
+		b.all_lights = s->all_lights_for(lv.front().first, hits, light_major_below);
 		for (int k = 0; k < b.n; k++) {
 			b.level[k] = lv[k].first;
 			b.nh[k] = lv[k].second;
@@ -475,6 +483,7 @@ struct Render {
 		k.io = ln.io;
 		k.direct_levels = direct_levels;
 		k.deep_split = deep_split;
+		k.light_major_below = light_major_below;
 		k.work_stats = s->ds.work_stats;
 		k.n0 = ln.n0;
 		k.rows_hash = ln.rows_hash;
@@ -499,7 +508,7 @@ struct Render {
 		b.dev_counts = 1;
 		int64_t hits = 0;
 		for (int L : lv) hits += pl.hits[L];
-		b.all_lights = s->all_lights_for(lv.front(), hits);
+		b.all_lights = s->all_lights_for(lv.front(), hits, light_major_below);
 		for (int k = 0; k < b.n; k++) {
 			const rtamd::RayLevel& L = ln.levels[lv[k]].lv;
 			b.level[k] = lv[k];
@@ -1117,7 +1126,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
-	if (const char* lm = std::getenv("RTAMD_LIGHT_MAJOR_BELOW")) s->light_major_below = std::atoll(lm);
+	if (const char* lm = std::getenv("RTAMD_LIGHT_MAJOR_BELOW"))
+		s->light_major_below_single = s->light_major_below_batch = std::atoll(lm);
 	if (const char* os = std::getenv("RTAMD_ONE_STREAM_PIXELS")) s->one_stream_pixels = std::atoll(os);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
@@ -1138,6 +1148,9 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 		rt_scene_destroy(s.release());
 		return rc;
 	}
+	// light-major single frames pay off where a shadow ray is a long LBVH search; a scene of
+	// spheres only keeps the batch threshold (C2a, one sphere and 5 lights: 0.183 vs 0.217 ms)
+	if (fs.face_geo.empty()) s->light_major_below_single = s->light_major_below_batch;
 	{
 		std::vector<rtamd::DCamera> cam(1, fs.camera);
 		if ((rc = upload(s.get(), cam, &s->ds.cam))) {
@@ -1390,6 +1403,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	Render R{s};
 	R.direct_levels = batch ? s->direct_levels_batch : s->direct_levels_single;
 	R.deep_split = batch ? s->deep_split_batch : s->deep_split_single;
+	R.light_major_below = batch ? s->light_major_below_batch : s->light_major_below_single;
 	R.progress = progress;
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
 	// the caller's stream is joined first (its prior work, e.g. the allocation of the
