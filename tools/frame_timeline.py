@@ -8,7 +8,7 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 
 
 def name(r):
-    m = re.search(r"(k_[a-z0-9_]+(?:<[a-z]+>)?)\(", r["Kernel_Name"])
+    m = re.search(r"(k_[a-z0-9_]+(?:<[a-z, ]+>)?)\(", r["Kernel_Name"])
     return m.group(1) if m else r["Kernel_Name"][:20]
 
 
