@@ -242,6 +242,7 @@ struct rt_scene {
 	// RTAMD_ONE_STREAM_PIXELS: a replayed chunk of at most this many pixels is issued on one
 	// stream (Render::issue_plan)
 	int64_t one_stream_pixels = (int64_t)1 << 17;
+	int one_stream_level1 = 1;  // RTAMD_ONE_STREAM_LEVEL1: a plan of one traced level on one stream too
 	int all_lights_for(int first_level, int64_t hits, int64_t light_major_below) const {
 		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
 		if (al && ds.n_nonambient > 1 && hits < light_major_below) al = 0;
@@ -560,7 +561,10 @@ struct Render {
 		// the chain, then every level's shading in one batch, then the reductions.  Waits across
 		// queues cost 6-19 us each between kernels of a few us (profiles/round3 timelines); a
 		// large chunk's overlap of shading and tracing is worth them, a small one's is not.
-		if (ln.n0 <= s->one_stream_pixels) {
+		// A plan of one traced level (no bounce: bdepth 0, or nothing reflective was hit) has
+		// nothing to overlap either: C2a 0.185 -> 0.179, C2b 0.334 -> 0.327, C4 0.357 -> 0.355 ms,
+		// C4 2-way share 0.302 -> 0.290 ms (RTAMD_ONE_STREAM_LEVEL1)
+		if (ln.n0 <= s->one_stream_pixels || (nlev == 1 && s->one_stream_level1)) {
 			for (int L = 0; L < nlev && rc == RT_OK; L++) {
 				const int remaining = depth - L;
 				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
@@ -1129,6 +1133,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* lm = std::getenv("RTAMD_LIGHT_MAJOR_BELOW"))
 		s->light_major_below_single = s->light_major_below_batch = std::atoll(lm);
 	if (const char* os = std::getenv("RTAMD_ONE_STREAM_PIXELS")) s->one_stream_pixels = std::atoll(os);
+	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
 	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);

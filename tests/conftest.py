@@ -13,6 +13,7 @@ os.environ.setdefault("RTAMD_LIGHT_MAJOR_BELOW", "0")
 # likewise the one-stream issue of small replayed chunks (api.cpp one_stream_pixels): off by
 # default so the multi-stream schedule stays covered; odd fuzz seeds and a knob test run it
 os.environ.setdefault("RTAMD_ONE_STREAM_PIXELS", "0")
+os.environ.setdefault("RTAMD_ONE_STREAM_LEVEL1", "0")  # and of plans of one traced level
 for p in (os.path.join(REPO, "cs184-raytracer_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

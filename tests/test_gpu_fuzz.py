@@ -104,6 +104,7 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
     # odd seeds: the production light-major threshold (every launch here is below it)
     monkeypatch.setenv("RTAMD_LIGHT_MAJOR_BELOW", "131072" if seed % 2 else "0")
     monkeypatch.setenv("RTAMD_ONE_STREAM_PIXELS", "131072" if seed % 2 else "0")
+    monkeypatch.setenv("RTAMD_ONE_STREAM_LEVEL1", "1" if seed % 2 else "0")
     path, bdepth, io = random_scene(seed, tmp_path)
     w, h = _W, _H
     try:
