@@ -1165,9 +1165,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	}
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_may_raise = fs.n_may_raise;
-	s->ds.treelet_root = fs.treelet_root;
 	if (const char* ws = std::getenv("RTAMD_WORK_STATS")) s->force_work_stats = std::atoi(ws) != 0;
-	s->ds.treelet_count = std::min(fs.treelet_count, rtamd::kTreeletNodes);
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	// j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
 	std::vector<int32_t> shadow_light;

@@ -14,22 +14,6 @@
 #ifndef RT_SAH_BINS
 #define RT_SAH_BINS 32
 #endif
-// Leaf termination (RT_SAH_LEAF 1): a set of at most RT_LEAF_MAX faces becomes a leaf when
-// its SAH cost n * CI is no more than splitting it, CT + (A_L n_L + A_R n_R) / A * CI;
-// 0: every set of more than kLeafFaces faces is split, smaller ones are leaves.
-#ifndef RT_SAH_LEAF
-#define RT_SAH_LEAF 0
-#endif
-#ifndef RT_LEAF_MAX
-#define RT_LEAF_MAX 7
-#endif
-#ifndef RT_SAH_CT
-#define RT_SAH_CT 1.0
-#endif
-#ifndef RT_SAH_CI
-#define RT_SAH_CI 1.5
-#endif
-
 namespace rtamd {
 namespace {
 
@@ -170,23 +154,7 @@ struct Builder {
 		max_depth = std::max(max_depth, depth);
 		Ref r;
 		r.box.empty();
-		int m = -1;
-		bool leaf = e - b <= kLeafFaces;
-		if (RT_SAH_LEAF && sah && !median_only) {
-			static_assert(RT_LEAF_MAX <= 7, "leaf face counts are 3-bit fields of the traversal's references");
-			leaf = e - b <= 1;
-			if (!leaf) {
-				double split_cost = INFINITY;
-				m = sah_split(b, e, &split_cost);
-				if (e - b <= RT_LEAF_MAX) {
-					Box all;
-					all.empty();
-					for (int i = b; i < e; i++) all.grow(boxes[order[i]]);
-					const double a = area(all);
-					leaf = !(a > 0) || (e - b) * RT_SAH_CI * a <= RT_SAH_CT * a + RT_SAH_CI * split_cost;
-				}
-			}
-		}
+		const bool leaf = e - b <= kLeafFaces;
 		if (leaf) {
 			r.first = static_cast<int32_t>(leaf_order.size());
 			r.count = e - b;
@@ -198,7 +166,7 @@ struct Builder {
 		}
 		const int idx = static_cast<int>(nodes.size());
 		nodes.emplace_back();
-		if (m < 0) m = (sah && !median_only) ? sah_split(b, e) : split(b, e);
+		const int m = (sah && !median_only) ? sah_split(b, e) : split(b, e);
 		const Ref c[2] = {build(b, m, depth + 1), build(m, e, depth + 1)};
 		DBvhNode& n = nodes[idx];
 		std::memset(&n, 0, sizeof(n));
@@ -217,55 +185,9 @@ struct Builder {
 	}
 };
 
-// Treelet layout: the top inner nodes of a mesh's LBVH renumbered into
-// breadth-first order right after its root, so that nodes [root, root + n) are the mesh's top
-// levels; the per-lane traversal reads those from a copy in LDS.  Only the node numbering
-// changes (child references follow it): boxes, leaves and every result are unchanged.
-int treelet_order(std::vector<DBvhNode>& nodes, size_t base, int max_nodes) {
-	const size_t n = nodes.size() - base;
-	if (n == 0) return 0;
-	std::vector<int32_t> bfs;  // local indices in breadth-first order (inner nodes only)
-	bfs.push_back(0);
-	for (size_t k = 0; k < bfs.size() && static_cast<int>(bfs.size()) < max_nodes; k++) {
-		const DBvhNode& nd = nodes[base + bfs[k]];
-		for (int c = 0; c < 2 && static_cast<int>(bfs.size()) < max_nodes; c++)
-			if (nd.count[c] == 0) bfs.push_back(nd.first[c] - static_cast<int32_t>(base));
-	}
-	std::vector<int32_t> to_new(n, -1);
-	int32_t next = 0;
-	for (int32_t v : bfs) to_new[v] = next++;
-	for (size_t v = 0; v < n; v++)
-		if (to_new[v] < 0) to_new[v] = next++;
-	std::vector<DBvhNode> old(nodes.begin() + base, nodes.end());
-	for (size_t v = 0; v < n; v++) {
-		DBvhNode nd = old[v];
-		for (int c = 0; c < 2; c++)
-			if (nd.count[c] == 0) nd.first[c] = static_cast<int32_t>(base) + to_new[nd.first[c] - static_cast<int32_t>(base)];
-		nodes[base + to_new[v]] = nd;
-	}
-	return static_cast<int>(bfs.size());
-}
-
 // Padded world-space box of an object-space box (the eight corners through fwd).  Used
 // only to skip geometries a ray cannot hit; a degenerate transform disables it.
-// The fp32 world box of the device's world cull (intersect.h world_slab32): the padded box
-// widened by 2^-20 of its largest coordinate, rounded outward (infinite bounds stay infinite).
-void world_box32(DGeom& d, double amax) {
-	const double pad = 0x1p-20 * amax;
-	for (int k = 0; k < 3; k++) {
-		d.wlo32[k] = std::isfinite(d.wlo[k]) ? round_down_f32(d.wlo[k] - pad) : static_cast<float>(d.wlo[k]);
-		d.whi32[k] = std::isfinite(d.whi[k]) ? round_up_f32(d.whi[k] + pad) : static_cast<float>(d.whi[k]);
-	}
-}
-
-void world_box_impl(const Geometry& g, const double lo[3], const double hi[3], DGeom& d, double& amax);
 void world_box(const Geometry& g, const double lo[3], const double hi[3], DGeom& d) {
-	double amax = 0;
-	world_box_impl(g, lo, hi, d, amax);
-	world_box32(d, amax);
-}
-
-void world_box_impl(const Geometry& g, const double lo[3], const double hi[3], DGeom& d, double& amax) {
 	bool finite = std::isfinite(g.det) && g.det != 0;
 	for (int i = 0; i < 3; i++)
 		for (int j = 0; j < 4; j++) finite = finite && std::isfinite(g.fwd.m[i][j]) && std::isfinite(g.inv.m[i][j]);
@@ -282,7 +204,7 @@ void world_box_impl(const Geometry& g, const double lo[3], const double hi[3], D
 		return;
 	}
 	double wl[3] = {INFINITY, INFINITY, INFINITY}, wh[3] = {-INFINITY, -INFINITY, -INFINITY};
-	amax = 0;
+	double amax = 0;
 	for (int c = 0; c < 8; c++) {
 		const double p[4] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2], 1.0};
 		double w[4];
@@ -298,43 +220,6 @@ void world_box_impl(const Geometry& g, const double lo[3], const double hi[3], D
 		d.wlo[k] = wl[k] - pad;
 		d.whi[k] = wh[k] + pad;
 	}
-}
-
-// World-space bounding sphere of a sphere geometry (intersect.h sphere_cull): centre fwd(c),
-// radius sqrt(rr) * sigma, sigma an upper bound of the largest singular value of fwd's 3x3
-// part (Gershgorin on M^T M: exact for a rotation times a uniform scale), padded relatively by
-// 1e-6 and by 1e-9 of the centre's magnitude.  Only ever used to skip the geometry.
-void world_sphere(const Geometry& g, DGeom& d) {
-	d.wr = -1.0;
-	bool finite = std::isfinite(g.det) && g.det != 0;
-	for (int i = 0; i < 3; i++)
-		for (int j = 0; j < 4; j++) finite = finite && std::isfinite(g.fwd.m[i][j]);
-	if (!finite || !(d.rr >= 0) || !std::isfinite(d.rr)) return;
-	double A[3][3];
-	for (int i = 0; i < 3; i++)
-		for (int j = 0; j < 3; j++) {
-			A[i][j] = 0;
-			for (int k = 0; k < 3; k++) A[i][j] += g.fwd.m[k][i] * g.fwd.m[k][j];
-		}
-	double lam = 0;
-	for (int i = 0; i < 3; i++) {
-		double r = A[i][i];
-		for (int j = 0; j < 3; j++)
-			if (j != i) r += std::fabs(A[i][j]);
-		lam = std::max(lam, r);
-	}
-	const double c4[4] = {g.center[0], g.center[1], g.center[2], 1.0};
-	double w[4];
-	affine_apply(g.fwd, c4, w);
-	double cmax = 0;
-	for (int k = 0; k < 3; k++) {
-		d.wc[k] = w[k];
-		cmax = std::max(cmax, std::fabs(w[k]));
-	}
-	const double r = std::sqrt(d.rr) * std::sqrt(lam) * (1.0 + 1e-6) + 1e-9 * cmax + 1e-300;
-	if (!std::isfinite(r) || !std::isfinite(cmax)) return;
-	d.wr = r;
-	d.wr2 = r * r * (1.0 + 1e-12);
 }
 
 // True unless every unit world direction is certain to keep a component above 1e-12 in
@@ -452,7 +337,6 @@ FlatScene flatten_scene(const Scene& s) {
 			const double lo[3] = {g.center[0] - rad, g.center[1] - rad, g.center[2] - rad};
 			const double hi[3] = {g.center[0] + rad, g.center[1] + rad, g.center[2] + rad};
 			world_box(g, lo, hi, d);
-			world_sphere(g, d);
 			fs.geoms.push_back(d);
 			continue;
 		}
@@ -557,13 +441,6 @@ FlatScene flatten_scene(const Scene& s) {
 			break;
 		}
 		d.bvh_root = static_cast<int32_t>(node_base);
-		const int tl = treelet_order(fs.nodes, node_base, kTreeletNodes);
-		// the scene's treelet: the top levels of its largest LBVH mesh
-		if (g.face_count > fs.treelet_faces) {
-			fs.treelet_faces = g.face_count;
-			fs.treelet_root = d.bvh_root;
-			fs.treelet_count = tl;
-		}
 		fs.geoms.push_back(d);
 	}
 	// shadow-test order: spheres and linear meshes first, then BVH meshes by size

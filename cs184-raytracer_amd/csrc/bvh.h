@@ -22,10 +22,6 @@ struct FlatScene {
 	int32_t n_may_raise = 0;
 	DCamera camera;
 	int max_bvh_depth = 0;
-	// the treelet (bvh.cpp treelet_order): nodes [treelet_root, treelet_root + treelet_count)
-	// are the top levels of the largest LBVH mesh, breadth-first
-	int32_t treelet_root = -1, treelet_count = 0;
-	int64_t treelet_faces = 0;
 };
 
 // Flattens the host scene, building an LBVH for every mesh with > kLinearFaces faces.

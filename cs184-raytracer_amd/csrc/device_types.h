@@ -27,12 +27,6 @@ constexpr int kLeafFaces = RT_LEAF_FACES;  // faces per LBVH leaf
 #define RT_STACK_DEPTH 32
 #endif
 constexpr int kStackDepth = RT_STACK_DEPTH;  // traversal stack entries per lane (LDS); LBVH depth <= kStackDepth - 2
-// top inner nodes of the largest LBVH mesh copied into every per-lane traversal block's LDS
-// (4 levels: 960 B); 0 disables the treelet
-#ifndef RT_TREELET_NODES
-#define RT_TREELET_NODES 0
-#endif
-constexpr int kTreeletNodes = RT_TREELET_NODES;
 
 struct alignas(16) DGeom {
 	double fwd[3][4];     // forwardTransform rows
@@ -51,13 +45,9 @@ struct alignas(16) DGeom {
 	// "ray has no direction" (rtbase.h:17-23): every ray must then check this geometry,
 	// even where culling or an early exit would skip it (bvh.cpp, intersect.h).
 	int32_t may_raise;
-	// the world box padded by 2^-20 of its largest coordinate and rounded outward to fp32
-	// (the fp32 world cull, intersect.h world_slab32)
-	float wlo32[3], whi32[3];
-	// spheres: a world-space bounding sphere (centre, radius and its square, padded; radius
-	// -1: none) for the cull of intersect.h sphere_cull (tighter than the box for a sphere)
-	double wc[3], wr, wr2;
+	int32_t pad[3];
 };
+static_assert(sizeof(DGeom) == 368, "geometry record: 368 B");
 
 struct alignas(16) DMaterial {   // rtbase.h:30-39
 	double ka[3], kd[3], ks[3], kr[3], kt[3];

@@ -12,9 +12,6 @@
 // Acceleration (new design, exact): LBVH per mesh, world-space boxes per geometry, and
 // conservative pre-tests that only ever skip work whose outcome is already decided.
 #pragma once
-#ifndef RT_SPECULATIVE
-#define RT_SPECULATIVE 1
-#endif
 #ifndef RT_PHASE_PROF
 #define RT_PHASE_PROF 0
 #endif
@@ -24,15 +21,6 @@
 // occluded_packet decides nothing (returns false after the may-raise check).
 #ifndef RT_DIAG_SKIP
 #define RT_DIAG_SKIP 0
-#endif
-// Facing pre-test (face_facing_rejects): exact skip of a face whose facing test certainly
-// fails, before its fp64 Cramer test.  0: off (A/B builds).  (A planar-geometry form, one
-// world-space dot product per geometry before its transform, measured -1.4 %: DESIGN.md.)
-#ifndef RT_FACE_ONE_FETCH
-#define RT_FACE_ONE_FETCH 1
-#endif
-#ifndef RT_FACING
-#define RT_FACING 1
 #endif
 #include <hip/hip_runtime.h>
 #include <cmath>
@@ -87,62 +75,12 @@ __device__ __forceinline__ double dot4z(V3 a, V3 b) { return (a.x * b.x + a.z * 
 __device__ __forceinline__ double sq4(V3 a) { return (a.x * a.x + a.z * a.z) + a.y * a.y; }
 // isZero(): all |c| <= 1e-12 (w is zero)
 __device__ __forceinline__ bool is_zero3(V3 a) { return fabs(a.x) <= 1e-12 && fabs(a.y) <= 1e-12 && fabs(a.z) <= 1e-12; }
-// Exact binary64 division with a shared divisor (RT_SHARED_DIV).  The compiler expands
-// every `a / b` into v_div_scale x2, v_rcp_f64, two Newton steps, a product, a residual,
-// v_div_fmas and v_div_fixup (11 instructions), and recomputes the reciprocal for each
-// quotient because v_div_scale depends on the numerator.  When neither operand needs
-// v_div_scale's scaling and the quotient is normal (|a|, |b| in [2^-300, 2^300]: exponent
-// gap < 768, no denormal 1/b or a/b, numerator exponent > 53) v_div_scale returns its operand
-// unchanged with VCC clear, v_div_fmas is a plain fma and v_div_fixup returns its input, so
-//   r = rcp(b); r = fma(r, fma(-b, r, 1), r) twice; q0 = a * r; q = fma(fma(-b, q0, a), r, q0)
-// is the hardware sequence itself, bit for bit, with r computed once per divisor (3
-// instructions per further quotient).  Any other operand takes the compiler's division.
-#ifndef RT_SHARED_DIV
-#define RT_SHARED_DIV 0
-#endif
-struct Recip {
-	double b, r;
-	bool ok;  // b in the range above
-};
-__device__ __forceinline__ bool div_range(double x) {
-	const double f = fabs(x);
-	return f >= 0x1p-300 && f <= 0x1p300;
-}
-__device__ __forceinline__ Recip recip(double b) {
-	Recip R;
-	R.b = b;
-	R.ok = RT_SHARED_DIV && div_range(b);
-	double r = __builtin_amdgcn_rcp(b);
-	r = fma(r, fma(-b, r, 1.0), r);
-	r = fma(r, fma(-b, r, 1.0), r);
-	R.r = r;
-	return R;
-}
-__device__ __forceinline__ double qdiv(double a, const Recip& R) {
-	if (__builtin_expect(R.ok && div_range(a), 1)) {
-		const double q0 = a * R.r;
-		return fma(fma(-R.b, q0, a), R.r, q0);
-	}
-	return a / R.b;
-}
 __device__ __forceinline__ V3 div3(V3 a, double n) { return mk(a.x / n, a.y / n, a.z / n); }
 // a.normalized() = a / |a| (Eigen divides by the norm): sqrt of ((x^2 + z^2) + y^2), then
-// three quotients sharing the divisor.  One decision for all three: the norm's square in
-// [2^-600, 2^600] puts the divisor in range, and a nonzero square of every component puts it
-// above 2^-538 (so |a_i / n| >= 2^-838; |a_i| <= n bounds it above); a zero component (its
-// sign of zero) or any other case takes the compiler's divisions.
+// three quotients sharing the divisor
 __device__ __forceinline__ V3 normalized3(V3 a, double* norm = nullptr) {
-	const double xx = a.x * a.x, yy = a.y * a.y, zz = a.z * a.z;
-	const double n2 = (xx + zz) + yy;  // sq4 (w == 0)
-	const double n = sqrt(n2);
+	const double n = sqrt((a.x * a.x + a.z * a.z) + a.y * a.y);  // sq4 (w == 0)
 	if (norm) *norm = n;
-	if (RT_SHARED_DIV && n2 >= 0x1p-600 && n2 <= 0x1p600 && xx != 0 && yy != 0 && zz != 0) {
-		double r = __builtin_amdgcn_rcp(n);
-		r = fma(r, fma(-n, r, 1.0), r);
-		r = fma(r, fma(-n, r, 1.0), r);
-		const double qx = a.x * r, qy = a.y * r, qz = a.z * r;
-		return mk(fma(fma(-n, qx, a.x), r, qx), fma(fma(-n, qy, a.y), r, qy), fma(fma(-n, qz, a.z), r, qz));
-	}
 	return div3(a, n);
 }
 
@@ -206,16 +144,12 @@ __device__ bool hits_bounding_box(V3 o, V3 d, P mn, P mx) {
 // only by the kernels instantiated with kCount (rt_render_params::work_stats): counting
 // costs 6% of the traversal kernels' time, so renders that do not ask for
 // the counts run kernels without them (WorkStats<false>: every member a no-op, reads 0).
-// RT_STATS_LDS: the counters live in the block's LDS, one slot per lane, and are bumped
-// with ds_add (five fewer VGPRs in the traversal loops, where every VGPR counts).
-#ifndef RT_STATS_LDS
-#define RT_STATS_LDS 1
-#endif
+// The counters live in the block's LDS, one slot per lane, bumped with ds_add (fewer VGPRs in
+// the traversal loops, where every VGPR counts).
 enum WorkCounter : int { W_NODES = 0, W_TRIS, W_CANDS, W_SPHERES, W_ENTRIES, W_COUNT };
 template <bool kCount>
 struct WorkStats {
 	static constexpr bool kOn = kCount;
-#if RT_STATS_LDS
 	uint32_t* c;  // this lane's counters: c[k * kBlock]
 	__device__ __forceinline__ void init(uint32_t* lds) {
 		if constexpr (kCount) {
@@ -236,20 +170,6 @@ struct WorkStats {
 		if constexpr (kCount) return c[k * kBlock];
 		return 0;
 	}
-#else
-	uint32_t c[W_COUNT];
-	__device__ __forceinline__ void init(uint32_t*) {
-#pragma unroll
-		for (int k = 0; k < W_COUNT; k++) c[k] = 0;
-	}
-	__device__ __forceinline__ void inc(int k) {
-		if constexpr (kCount) c[k]++;
-	}
-	__device__ __forceinline__ void add(int k, bool b) {
-		if constexpr (kCount) c[k] += b;
-	}
-	__device__ __forceinline__ uint32_t get(int k) const { return kCount ? c[k] : 0; }
-#endif
 #if RT_PHASE_PROF
 	uint32_t ph[kPhaseSlots];  // shader-clock cycles per phase while this lane was active
 #endif
@@ -358,59 +278,40 @@ __device__ __forceinline__ bool face_facing_rejects(FP F, V3 d, bool reverse) {
 // strictly closer, or equally close with a smaller reference index: over any visiting
 // order this selects the same face as the reference's in-order scan.
 // Returns true when kAnyHit and the face passes (the caller's question is answered).
-template <bool kAnyHit, bool kUniform = false, typename WS>
+// Per lane (the packet traversal uses test_face_pred): the vertices are fetched only for
+// faces the facing pre-test keeps.
+template <bool kAnyHit, typename WS>
 __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn, bool reverse,
                                           double any_limit, MeshBest& best, WS& ws) {
 	ws.inc(W_TRIS);
-	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
-	// A wave-uniform record (RT_FACE_ONE_FETCH): vertices, id and cone in one round of scalar
-	// loads before the facing pre-test, else the vertices wait for a second memory round
-	// trip after it.  Per lane, the vertices are fetched only for faces the pre-test keeps.
-	constexpr bool kEarly = kUniform && RT_FACE_ONE_FETCH;
-	V3 p0, va, vb;
-	int32_t id;
-	if constexpr (kEarly) {
-		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-		id = F->id;
-		const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
-		asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
-		             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
-		if (RT_FACING && facing_rejects(c0, c1, c2, tau, d, reverse)) return false;
-	} else if (RT_FACING && face_facing_rejects(F, d, reverse)) {
-		return false;
-	}
-	if constexpr (!kEarly) {
-		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-		// id is fetched with the vertices: the compiler would otherwise issue its load where
-		// it is first used (one more memory round trip per candidate face)
-		id = F->id;
-		if constexpr (kUniform)
-			asm volatile("" ::"s"(id));  // materialised here: no separate fetch at its first use
-		else
-			asm volatile("" ::"v"(id));
-	}
+	const DFaceGeo* F = S.fgeo + f;
+	if (face_facing_rejects(F, d, reverse)) return false;
+	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	// id is fetched with the vertices: the compiler would otherwise issue its load where it is
+	// first used (one more memory round trip per candidate face)
+	const int32_t id = F->id;
+	asm volatile("" ::"v"(id));
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	if (D == 0) return false;
 	const double Da = det3(rhs, vb, nd);
 	if (quotient_surely_negative(Da, D) || quotient_surely_above(Da, D, 1.0)) return false;
-	const Recip RD = recip(D);  // Cramer's three quotients share the divisor
-	const double a = qdiv(Da, RD);
+	const double a = Da / D;
 	if (a < 0 || a > 1) return false;
 	const double Db = det3(va, rhs, nd);
 	if (quotient_surely_negative(Db, D) || quotient_surely_above(Db, D, 1.0)) return false;
-	const double b = qdiv(Db, RD);
+	const double b = Db / D;
 	if (b < 0 || a + b > 1) return false;
 	const double Dt = det3(va, vb, rhs);
 	if (quotient_surely_negative(Dt, D)) return false;
 	// dist = t * dn with dn = |d|_3 within a few ulps of 1: t > 1.001 * best * 1.001 cannot win
 	if (best.dist < INFINITY && best.dist >= 0x1p-900 && quotient_surely_above(Dt, D, best.dist * 1.001)) return false;
-	const double t = qdiv(Dt, RD);
+	const double t = Dt / D;
 	if (t < 0) return false;
 	const double dist = t * dn;
 	if (!(dist < best.dist || (dist == best.dist && id < best.id))) return false;
 	ws.inc(W_CANDS);
-	const V3 tn = face_normal<kUniform>(S, f, a, b);
+	const V3 tn = face_normal(S, f, a, b);
 	const bool front = dot4z(tn, d) < 0;
 	if (!front ^ reverse) return false;
 	best.dist = dist;
@@ -421,52 +322,28 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 	return kAnyHit && dist < any_limit;
 }
 
-// The wave-packet form of test_face (RT_PRED_FACE): the same decisions, but each lane's
-// early exits become a running predicate and the wave leaves only when no lane is left
-// (a wave-uniform branch).  The branchy form pays exec-mask bookkeeping (s_and_saveexec,
-// s_cbranch_execz, the join) at every exit of every face test, in a kernel whose
-// instruction stream is as much scalar as vector; here a lane that has failed just
-// computes along, its results never selected.  Divisions of failed lanes may see D = 0
-// (inf/NaN, discarded).  Returns, per lane, kAnyHit && the face passes within any_limit.
-#ifndef RT_PRED_FACE
-#define RT_PRED_FACE 1
-#endif
-// RT_PACKET_TOP: the packet traversal keeps its stack's most recent push in a scalar register,
-// so popping it needs no LDS round trip before the next node's record is requested
-#ifndef RT_PACKET_TOP
-#define RT_PACKET_TOP 0
-#endif
-#ifndef RT_PRED_FACE_LANE
-#define RT_PRED_FACE_LANE 0
-#endif
+// The wave-packet form of test_face: the same decisions, but each lane's early exits
+// become a running predicate and the wave leaves only when no lane is left (a wave-uniform
+// branch).  The branchy form pays exec-mask bookkeeping (s_and_saveexec, s_cbranch_execz,
+// the join) at every exit of every face test, in a kernel whose instruction stream is as
+// much scalar as vector; here a lane that has failed just computes along, its results never
+// selected.  Divisions of failed lanes may see D = 0 (inf/NaN, discarded).  The range tests
+// keep the reference's form (geometry.cpp:93-106: a NaN a, b or t is not rejected there).
+// Returns, per lane, kAnyHit && the face passes within any_limit.
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
-// kUniform false (RT_PRED_FACE_LANE): the per-lane LBVH search's form, each lane on a face
-// of its own leaf (f must index a face for every lane, `on` or not); the vertices are
-// fetched after the facing pre-test, as in test_face.
-template <bool kAnyHit, bool kUniform = true, typename WS>
+template <bool kAnyHit, typename WS>
 __device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn,
                                                bool reverse, double any_limit, MeshBest& best, WS& ws,
                                                bool on) {
 	ws.add(W_TRIS, on);
-	const auto F = scene_ptr<kUniform>(S.fgeo) + f;
-	V3 p0, va, vb;
-	int32_t id;
-	bool ok;
-	if constexpr (kUniform) {
-		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-		id = F->id;
-		const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
-		asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
-		             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
-		ok = on && !(RT_FACING && facing_rejects(c0, c1, c2, tau, d, reverse));
-		if (!wave_any(ok)) return false;
-	} else {
-		ok = on && !(RT_FACING && face_facing_rejects(F, d, reverse));
-		if (!wave_any(ok)) return false;
-		p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
-		id = F->id;
-		asm volatile("" ::"v"(id));
-	}
+	const auto F = uniform_ptr(S.fgeo) + f;
+	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
+	const int32_t id = F->id;
+	const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
+	asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
+	             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
+	bool ok = on && !facing_rejects(c0, c1, c2, tau, d, reverse);
+	if (!wave_any(ok)) return false;
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	const double Da = det3(rhs, vb, nd);
@@ -474,20 +351,20 @@ __device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, 
 	if (!wave_any(ok)) return false;
 	const double a = Da / D;
 	const double Db = det3(va, rhs, nd);
-	ok = ok && a >= 0 && a <= 1 && !quotient_surely_negative(Db, D) && !quotient_surely_above(Db, D, 1.0);
+	ok = ok && !(a < 0 || a > 1) && !quotient_surely_negative(Db, D) && !quotient_surely_above(Db, D, 1.0);
 	if (!wave_any(ok)) return false;
 	const double b = Db / D;
 	const double Dt = det3(va, vb, rhs);
 	// dist = t * dn with dn = |d|_3 within a few ulps of 1: t > 1.001 * best * 1.001 cannot win
 	const bool beyond = best.dist < INFINITY && best.dist >= 0x1p-900 && quotient_surely_above(Dt, D, best.dist * 1.001);
-	ok = ok && b >= 0 && a + b <= 1 && !quotient_surely_negative(Dt, D) && !beyond;
+	ok = ok && !(b < 0 || a + b > 1) && !quotient_surely_negative(Dt, D) && !beyond;
 	if (!wave_any(ok)) return false;
 	const double t = Dt / D;
 	const double dist = t * dn;
-	ok = ok && t >= 0 && (dist < best.dist || (dist == best.dist && id < best.id));
+	ok = ok && !(t < 0) && (dist < best.dist || (dist == best.dist && id < best.id));
 	if (!wave_any(ok)) return false;
 	ws.add(W_CANDS, ok);
-	const V3 tn = face_normal<kUniform>(S, f, a, b);
+	const V3 tn = face_normal<true>(S, f, a, b);
 	const bool front = dot4z(tn, d) < 0;
 	ok = ok && !(!front ^ reverse);
 	if (ok) {
@@ -527,20 +404,17 @@ __device__ __forceinline__ V3 safe_inv(V3 d) { return mk(slab_rcp(d.x), slab_rcp
 
 __device__ __forceinline__ double prune_limit(double best_dist) { return best_dist * (1.0 + 4e-9); }
 
-// Relative widening of the fp32 slab interval (round 1).  Not needed, per axis a (below):
-// the computed plane parameter fma(lo, I, -fl(o' I)) errs from (lo - o') / d_a by at most
-// 2^-23 |I| |o'_a| + 2^-23 |t| <= 1.5 * 2^-22 amax |I| (|o'_a|, |lo| <= amax, so |t| <= 2
-// amax |I|), while a face point inside the unpadded child box lies >= 2^-18 amax |I| in t
-// from each padded plane: the test keeps every box such a point is in, with a margin of
-// ten, without it.  1 restores the widening (A/B builds).
-#ifndef RT_SLAB32_WIDEN
-#define RT_SLAB32_WIDEN 0
-#endif
+// Per axis a, the computed plane parameter fma(lo, I, -fl(o' I)) errs from (lo - o') / d_a by
+// at most 2^-23 |I| |o'_a| + 2^-23 |t| <= 1.5 * 2^-22 amax |I| (|o'_a|, |lo| <= amax, so
+// |t| <= 2 amax |I|), while a face point inside the unpadded child box lies >= 2^-18 amax |I|
+// in t from each padded plane: the test keeps every box such a point is in, with a margin
+// of ten, without widening the interval (round 1's relative 2^-20 widening was dropped in
+// round 2, +1.7%).
 // fp32 node test.  The ray origin is first moved along the ray to where it enters the
 // mesh's box (o' = o + s d, s >= 0; no face lies before it), so |o'| <= amax, the largest
 // vertex coordinate magnitude; then t' = lo * I - o' * I in fp32 errs by at most about
 // 6 * 2^-24 * amax in position, far inside the 2^-18 * amax the node boxes are padded by
-// (bvh.cpp), and the relative 2^-22 in t' is inside it too (RT_SLAB32_WIDEN).  A ray that
+// (bvh.cpp), and the relative 2^-22 in t' is inside it too.  A ray that
 // misses the box finds no face whatever the node tests say.  |I| is clamped to 2^60:
 // for a direction component below 2^-60 the clamped distances to the padded planes still
 // exceed any face distance (the planes lie >= 2^-18 amax from every face).
@@ -576,35 +450,12 @@ __device__ __forceinline__ bool slab32(P lo, P hi, const Ray32& r, float lim, fl
 	const float tx0 = fmaf(lo[0], r.ix, -r.oix), tx1 = fmaf(hi[0], r.ix, -r.oix);
 	const float ty0 = fmaf(lo[1], r.iy, -r.oiy), ty1 = fmaf(hi[1], r.iy, -r.oiy);
 	const float tz0 = fmaf(lo[2], r.iz, -r.oiz), tz1 = fmaf(hi[2], r.iz, -r.oiz);
-	float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-	float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-	if (RT_SLAB32_WIDEN) {
-		tmin = fmaf(-fabsf(tmin), 0x1p-20f, tmin);
-		tmax = fmaf(fabsf(tmax), 0x1p-20f, tmax);
-	}
+	const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+	const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
 	tnear = tmin;
 	return tmax >= tmin && tmax >= 0.0f && tmin <= lim;
 }
 
-
-
-
-// The treelet (bvh.cpp treelet_order): the top inner nodes of the scene's largest LBVH mesh,
-// copied into LDS by every per-lane traversal block (load_treelet) and read from there by
-// mesh_search: the first levels of every descent cost an LDS read instead of a dependent L2
-// round trip.  (Module-scope LDS: allocated only in the kernels that reach mesh_search.)
-__shared__ DBvhNode g_treelet[kTreeletNodes > 0 ? kTreeletNodes : 1];
-
-__device__ __forceinline__ void load_treelet(const DeviceScene& S) {
-	if (kTreeletNodes > 0) {
-		constexpr int kPieces = sizeof(DBvhNode) / sizeof(uint4);
-		const int n = S.treelet_count * kPieces;
-		const uint4* src = reinterpret_cast<const uint4*>(S.nodes + (S.treelet_root < 0 ? 0 : S.treelet_root));
-		uint4* dst = reinterpret_cast<uint4*>(g_treelet);
-		for (int k = threadIdx.x; k < n; k += blockDim.x) dst[k] = src[k];
-	}
-	__syncthreads();
-}
 
 // A node record in registers: the child boxes and the child references
 struct NodeRec {
@@ -621,98 +472,14 @@ __device__ __forceinline__ void read_node(const DBvhNode* N, NodeRec& r) {
 		}
 	r.refs = *reinterpret_cast<const int4*>(N->first);
 }
-__device__ __forceinline__ void fetch_node(const DeviceScene& S, int32_t ref, NodeRec& r) {
-	const uint32_t tli = static_cast<uint32_t>(ref - S.treelet_root);
-	if (kTreeletNodes > 0 && tli < static_cast<uint32_t>(S.treelet_count))
-		read_node(g_treelet + tli, r);
-	else
-		read_node(S.nodes + ref, r);
-}
+__device__ __forceinline__ void fetch_node(const DeviceScene& S, int32_t ref, NodeRec& r) { read_node(S.nodes + ref, r); }
 
-// Bounding-sphere cull of sphere geometries (RT_SPHERE_CULL), instead of their world box.
-// With v = wc - o and b = v.d (d unit), a ray can meet the padded world sphere (wc, wr) on
-// [0, lim] only if its squared distance to the centre line q = v.v - b^2 <= wr^2 and
-// -wr <= b <= lim + wr.  The fp64 rounding of v, b and q errs by < 2^-47 |v|^2 in q and
-// < 2^-50 |v| in b; the slack 2^-40 v.v on q and eo = 2^-30 |o|_1 on b (with the host's
-// 1e-9 |wc| in wr) exceed both, so the test never drops a sphere the exact ray reaches.
-// A sphere's box admits rays through its corners (1.9x the sphere's volume); each one
-// the sphere test rejects saves an object-space transform, normalisation and quadratic.
-#ifndef RT_SPHERE_CULL
-#define RT_SPHERE_CULL 0
-#endif
-__device__ __forceinline__ double sphere_cull_slack(V3 o) { return 0x1p-30 * ((fabs(o.x) + fabs(o.y)) + fabs(o.z)); }
+// The world cull of geometry G: its padded world box (a ray that misses it, or enters it
+// beyond lim, cannot hit the geometry within lim)
 template <typename GP>
-__device__ __forceinline__ bool sphere_cull(GP G, V3 o, V3 d, double lim) {
-	const double eo = sphere_cull_slack(o);  // per test, not held per ray (register pressure)
-	const double vx = G->wc[0] - o.x, vy = G->wc[1] - o.y, vz = G->wc[2] - o.z;
-	const double b = (vx * d.x + vy * d.y) + vz * d.z;
-	const double vv = (vx * vx + vy * vy) + vz * vz;
-	const double rt = G->wr + eo;
-	return vv - b * b <= G->wr2 + 0x1p-40 * vv && b >= -rt && b <= lim + rt;
-}
-// The world cull of geometry G: its bounding sphere (spheres) or its padded box
-template <typename GP>
-__device__ __forceinline__ bool world_cull(GP G, V3 o, V3 d, V3 winv, double lim) {
-	if (RT_SPHERE_CULL && G->kind == DGEOM_SPHERE && G->wr >= 0.0) return sphere_cull(G, o, d, lim);
+__device__ __forceinline__ bool world_cull(GP G, V3 o, V3 winv, double lim) {
 	double tw;
 	return slab(G->wlo, G->whi, o, winv, lim, tw);
-}
-
-// World-space culling in fp32 (RT_WORLD32).  A geometry whose padded world box the ray
-// misses is skipped without its object-space transform; the test only ever skips geometries
-// the exact ray cannot reach, so its precision decides speed, not results.  In fp32:
-//   t = fma(L32, I, -(o32 I +- delta))  per plane, delta = 2^-19 |o|_inf |I_a|
-// The boxes are padded on the host by 2^-20 of their largest coordinate before rounding
-// outward to fp32 (bvh.cpp world_box32), which covers the 2^-22 relative error of I and of
-// L32 I; delta covers the 2^-21 relative error of o32 I (rounding o and the product); the
-// sign of I picks which plane's term is raised, so both slab ends move outward.  Far origins
-// (|o| >= 2^100, fp32 overflow) and NaN directions get infinite delta: never culled here.
-// Replaces round 2's fp64 slab (30 4-cycle instructions per geometry, 12 SGPRs per box in the
-// packet kernels) with 6 fp32 FMAs and the min/max tree (6 SGPRs per box).
-#ifndef RT_WORLD32
-#define RT_WORLD32 0
-#endif
-struct WorldRay32 {
-	float ix, iy, iz;     // I = 1/d, clamped to +-2^60
-	float olx, oly, olz;  // o32 I + delta sign(I): the lower planes' terms
-	float ohx, ohy, ohz;  // o32 I - delta sign(I): the upper planes' terms
-};
-__device__ __forceinline__ WorldRay32 world_ray32(V3 o, V3 d) {
-	WorldRay32 r;
-	const float inv[3] = {__builtin_amdgcn_rcpf(static_cast<float>(d.x)), __builtin_amdgcn_rcpf(static_cast<float>(d.y)),
-	                      __builtin_amdgcn_rcpf(static_cast<float>(d.z))};  // v_rcp_f32: 1 ulp
-	const float o32[3] = {static_cast<float>(o.x), static_cast<float>(o.y), static_cast<float>(o.z)};
-	const float omax = fmaxf(fmaxf(fabsf(o32[0]), fabsf(o32[1])), fabsf(o32[2]));
-	float I[3], lo[3], hi[3];
-#pragma unroll
-	for (int a = 0; a < 3; a++) {
-		// a NaN inverse stays NaN through the clamp's comparisons only if tested first
-		I[a] = (inv[a] == inv[a]) ? fminf(fmaxf(inv[a], -0x1p60f), 0x1p60f) : inv[a];
-		const float oi = o32[a] * I[a];
-		const float delta = (omax < 0x1p100f && I[a] == I[a]) ? 0x1p-19f * omax * fabsf(I[a]) : INFINITY;
-		const float sd = I[a] < 0.0f ? -delta : delta;
-		lo[a] = oi + sd;
-		hi[a] = oi - sd;
-	}
-	r.ix = I[0], r.iy = I[1], r.iz = I[2];
-	r.olx = lo[0], r.oly = lo[1], r.olz = lo[2];
-	r.ohx = hi[0], r.ohy = hi[1], r.ohz = hi[2];
-	return r;
-}
-// lim rounded up to fp32 (+inf stays +inf)
-__device__ __forceinline__ float world_lim32(double lim) {
-	float f = static_cast<float>(lim);
-	if (static_cast<double>(f) < lim) f = __uint_as_float(__float_as_uint(f) + (f >= 0.0f ? 1u : 0xffffffffu));
-	return f;
-}
-template <typename GP>
-__device__ __forceinline__ bool world_slab32(GP G, const WorldRay32& r, float lim) {
-	const float tx0 = fmaf(G->wlo32[0], r.ix, -r.olx), tx1 = fmaf(G->whi32[0], r.ix, -r.ohx);
-	const float ty0 = fmaf(G->wlo32[1], r.iy, -r.oly), ty1 = fmaf(G->whi32[1], r.iy, -r.ohy);
-	const float tz0 = fmaf(G->wlo32[2], r.iz, -r.olz), tz1 = fmaf(G->whi32[2], r.iz, -r.ohz);
-	const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-	const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-	return tmax >= tmin && tmax >= 0.0f && tmin <= lim;
 }
 
 // Mesh::calculateIntNormInObjSpace (geometry.cpp:69-126) with an LBVH in place of the
@@ -764,7 +531,6 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 		// still walking inner nodes postpones it (`leaf`) and keeps walking, so fewer lanes
 		// idle in either phase.  Any visiting order selects the same face (test_face).
 		int32_t leaf = -1;
-		bool occluded = false;  // RT_PRED_FACE_LANE: an any-hit face passed within any_limit
 		while (ref != -1 || leaf != -1) {
 			PROF_BEGIN(tn);
 			while (ref >= 0) {
@@ -793,45 +559,18 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 				} else {
 					ref = pop();
 				}
-				if (RT_SPECULATIVE && ref <= -2 && leaf == -1) {
+				if (ref <= -2 && leaf == -1) {
 					leaf = ref;
 					ref = pop();
 				}
-				if (RT_SPECULATIVE && __ballot(leaf == -1) == 0) break;  // every walking lane holds a leaf
+				if (__ballot(leaf == -1) == 0) break;  // every walking lane holds a leaf
 			}
 #if RT_DIAG_LANES
 			diag_lanes(kAnyHit ? 26 : 10, leaf != -1);  // lanes holding a leaf when the face phase starts
 #endif
 			PROF_END(ws, PH_NODES, tn);
-			if (!RT_SPECULATIVE && ref <= -2) {
-				leaf = ref;
-				ref = pop();
-			}
 			// the postponed leaf, then a leaf the walk stopped on
 			PROF_BEGIN(tf);
-#if RT_PRED_FACE_LANE
-			// the lanes holding a leaf test face k of it together, k up to the wave's largest
-			// leaf (test_face_pred); an occluded lane leaves the search (ref = leaf = -1)
-			while (wave_any(leaf != -1)) {
-				const int32_t code = leaf != -1 ? -2 - leaf : 0;
-				const int32_t fb = G->face_begin + (code >> 3);
-				int32_t cnt = code & 7;
-				for (int32_t k = 0; wave_any(k < cnt); k++) {
-					const bool on = k < cnt;
-					if (test_face_pred<kAnyHit, false>(S, on ? fb + k : fb, o, d, nd, dn, reverse, any_limit, best,
-					                                   ws, on)) {
-						occluded = true;
-						cnt = 0;
-						ref = -1;
-					}
-				}
-				leaf = -1;
-				if (ref <= -2) {
-					leaf = ref;
-					ref = pop();
-				}
-			}
-#else
 			while (leaf != -1) {
 				const int32_t code = -2 - leaf;
 				const int32_t f0 = G->face_begin + (code >> 3), f1 = f0 + (code & 7);
@@ -847,13 +586,8 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 					ref = pop();
 				}
 			}
-#endif
 			lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 			PROF_END(ws, PH_FACES, tf);
-		}
-		if (occluded) {
-			settled = true;
-			return true;
 		}
 	}
 	found_dist = best.dist;
@@ -943,20 +677,12 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
                             V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WS& ws) {
 	bool found = false;
 	FaceHit best{-1, 0, 0};
-#if RT_WORLD32
-	const WorldRay32 wr = world_ray32(o, d);
-#else
 	const V3 winv = safe_inv(d);
-#endif
 	check_may_raise(S, d, true, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
 		PROF_BEGIN(tw0);
-#if RT_WORLD32
-		const bool wb = world_slab32(G, wr, found ? world_lim32(prune_limit(best_dist)) : INFINITY);
-#else
-		const bool wb = world_cull(G, o, d, winv, found ? prune_limit(best_dist) : INFINITY);
-#endif
+		const bool wb = world_cull(G, o, winv, found ? prune_limit(best_dist) : INFINITY);
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wb) continue;
 		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
@@ -1043,23 +769,14 @@ __device__ __forceinline__ double shadow_slab_limit(double dist_light) {
 template <typename WS>
 __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, int32_t* stack,
                          DeviceCounters* ctr, WS& ws) {
-#if RT_WORLD32
-	const WorldRay32 wr = world_ray32(o, d);
-	const float lim = world_lim32(shadow_slab_limit(dist_light));
-#else
 	const V3 winv = safe_inv(d);
 	const double lim = shadow_slab_limit(dist_light);
-#endif
 	check_may_raise(S, d, true, ctr);
 	for (int k = 0; k < S.n_geoms; k++) {
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		PROF_BEGIN(tw0);
-#if RT_WORLD32
-		const bool wb = world_slab32(G, wr, lim);
-#else
-		const bool wb = world_cull(G, o, d, winv, lim);
-#endif
+		const bool wb = world_cull(G, o, winv, lim);
 		PROF_END(ws, PH_WORLD, tw0);
 		if (wb && geom_occludes(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
 	}
@@ -1097,11 +814,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 		if (G->bvh_root < 0) {
 			PROF_BEGIN(tf);
 			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++) {
-				bool hitf;
-				if (RT_PRED_FACE)
-					hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws, live);
-				else
-					hitf = live && test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws);
+				const bool hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws, live);
 				settled = settled || hitf;
 				live = live && !hitf;
 			}
@@ -1115,7 +828,6 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			const int32_t fbase = uniform_i32(G->face_begin);
 			int32_t node = uniform_i32(G->bvh_root);
 			int sp = 0;
-			int32_t top = -1;  // RT_PACKET_TOP: the stack's top entry (-1: none)
 			// the node record: the whole 64 B in one scalar load, both child boxes tested by
 			// every lane (a lane that is done ignores its results)
 			float box[2][2][3];  // [child][lo, hi][axis]
@@ -1156,19 +868,10 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				int32_t next = -1;
 				if (w_first && c_first == 0) next = f_first;
 				if (w_second && c_second == 0) {
-					if (next < 0) {
+					if (next < 0)
 						next = f_second;
-					} else if (RT_PACKET_TOP) {
-						// the stack's top entry in a scalar register: pushed below it to LDS
-						if (top >= 0 && sp < kStackDepth) wstack[sp++] = top;
-						top = f_second;
-					} else if (sp < kStackDepth) {
+					else if (sp < kStackDepth)
 						wstack[sp++] = f_second;  // LBVH depth <= kStackDepth - 2 (bvh.cpp)
-					}
-				}
-				if (RT_PACKET_TOP && next < 0 && top >= 0) {
-					next = top;  // no LDS round trip before the next node's fetch
-					top = -1;
 				}
 				if (next < 0 && sp > 0) next = uniform_i32(wstack[--sp]);
 				if (next >= 0) fetch(next);
@@ -1185,13 +888,8 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					PROF_BEGIN(tf);
 					const int32_t f0 = fbase + cf;
 					for (int32_t f = f0; f < f0 + cc; f++) {
-						bool hitf;
-						if (RT_PRED_FACE)
-							hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws,
-							                               __builtin_amdgcn_inverse_ballot_w64(want) && live);
-						else
-							hitf = __builtin_amdgcn_inverse_ballot_w64(want) && live &&
-							       test_face<kAnyHit, true>(S, f, o, d, nd, dn, reverse, any_limit, best, ws);
+						const bool hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws,
+						                                          __builtin_amdgcn_inverse_ballot_w64(want) && live);
 						settled = settled || hitf;
 						live = live && !hitf;
 					}
@@ -1223,20 +921,12 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
                                    WS& ws) {
 	bool found = false;
 	FaceHit best{-1, 0, 0};
-#if RT_WORLD32
-	const WorldRay32 wr = world_ray32(o, d);
-#else
 	const V3 winv = safe_inv(d);
-#endif
 	check_may_raise(S, d, on, ctr);
 	for (int g = 0; g < S.n_geoms; g++) {
 		const auto G = uniform_ptr(S.geoms) + g;
 		PROF_BEGIN(tw0);
-#if RT_WORLD32
-		const bool cand = on && world_slab32(G, wr, found ? world_lim32(prune_limit(best_dist)) : INFINITY);
-#else
-		const bool cand = on && world_cull(G, o, d, winv, found ? prune_limit(best_dist) : INFINITY);
-#endif
+		const bool cand = on && world_cull(G, o, winv, found ? prune_limit(best_dist) : INFINITY);
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
 		PROF_BEGIN(tx);
@@ -1276,12 +966,7 @@ template <typename WS>
 __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, bool on,
                                 int32_t* wstack, DeviceCounters* ctr, WS& ws) {
 	const bool inf_light = dist_light == INFINITY;
-#if RT_WORLD32
-	const WorldRay32 wr = world_ray32(o, d);
-	const float wlim = world_lim32(shadow_slab_limit(dist_light));
-#else
 	const V3 winv = safe_inv(d);
-#endif
 	bool occ = false;
 	check_may_raise(S, d, on, ctr);
 	if (RT_DIAG_SKIP & 4) return false;
@@ -1289,11 +974,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		PROF_BEGIN(tw0);
-#if RT_WORLD32
-		const bool cand = on && !occ && world_slab32(G, wr, wlim);
-#else
-		const bool cand = on && !occ && world_cull(G, o, d, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6));
-#endif
+		const bool cand = on && !occ && world_cull(G, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6));
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
 #if RT_DIAG_GEOMS

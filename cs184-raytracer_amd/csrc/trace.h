@@ -24,7 +24,6 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	int32_t n_geoms, n_lights, n_nonambient;
 	int32_t n_may_raise;                      // geometries with DGeom::may_raise
 	const int32_t* shadow_light;              // j-th non-ambient light -> light index
-	int32_t treelet_root, treelet_count;      // nodes [root, root + count) staged in LDS (per-lane traversal)
 	int32_t work_stats;                       // count the LBVH work (rt_counters node_visits ...); 0 = skip
 };
 

@@ -357,7 +357,6 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	if constexpr (!kPacket) load_treelet(S);
 	// level records read through the constant address space (scalar loads at their uses)
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -476,37 +475,10 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 //    towards each light in turn (one light at a time, still wave-uniform), loading the hit
 //    records once for all lights.
 // The light record of the wave is read with scalar loads.
-// Hit records of the packet shadow kernel staged in LDS (RT_HIT_LDS): the hit point and
-// normal (and the viewing direction of the fused shading) are read from the block's LDS for
-// every light and for the Phong terms instead of occupying 18 VGPRs through every traversal.
-#ifndef RT_HIT_LDS
-#define RT_HIT_LDS 0
-#endif
-typedef __attribute__((address_space(3))) double lds_f64;
-// an LDS address the compiler cannot see through: the values are read back from LDS, not
-// kept in registers from the store (which is what staging them avoids)
-__device__ __forceinline__ lds_f64* opaque_lds(lds_f64* p) {
-	asm volatile("" : "+v"(p));
-	return p;
-}
-struct HitStage {
-	lds_f64* p;  // this lane's slots: p[k * kBlock], k = 0..8 (P, N, d)
-	__device__ __forceinline__ void put(int k, V3 v) {
-		p[(3 * k + 0) * kBlock] = v.x;
-		p[(3 * k + 1) * kBlock] = v.y;
-		p[(3 * k + 2) * kBlock] = v.z;
-	}
-	__device__ __forceinline__ V3 get(int k) const {
-		const lds_f64* q = opaque_lds(p);
-		return mk(q[(3 * k + 0) * kBlock], q[(3 * k + 1) * kBlock], q[(3 * k + 2) * kBlock]);
-	}
-};
-
 template <bool kPacket, bool kCount>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
-                                            uint32_t* stat_lds, double* hit_lds) {
-	constexpr bool kStage = kPacket && RT_HIT_LDS;
+                                            uint32_t* stat_lds) {
 	const int nl = S.n_nonambient;
 	const BatchItem it = batch_item<true>(B, nl, tg);
 	const int level = it.level;
@@ -529,7 +501,6 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	const bool on = h < nh;
 	V3 P = mk(0, 0, 0), N = mk(0, 0, 1);
 	bool inside = false, zero_mat = false;
-	HitStage hs{(lds_f64*)(hit_lds) + threadIdx.x};
 	{
 		// the level's record, read here and again where the verdicts are written (opaque: its
 		// buffer pointers are not held in scalar registers through the traversals)
@@ -540,11 +511,6 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 			const uint8_t fl = cur.hinside[h];
 			inside = fl & 1;
 			zero_mat = fl & 2;
-			if constexpr (kStage) {
-				hs.put(0, P);
-				hs.put(1, N);
-				hs.put(2, mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]));
-			}
 		}
 	}
 	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
@@ -552,12 +518,6 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 		V3 Ld = mk(0, 0, 1);
 		bool rev = false, zero = false;
 		double dL = 0;
-		if constexpr (kStage) {
-			if (on) {
-				P = hs.get(0);
-				N = hs.get(1);
-			}
-		}
 		if (on) {
 			const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
 			const bool point = L.kind == DLIGHT_POINT;
@@ -572,13 +532,8 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 			// the light is occluded or not (it is never -0), so the ray is not traced.
 			if (zero_mat && L.zero_terms && nl_dot <= 0.0) {
 				const V3 R = (2 * nl_dot) * N - Ld;
-				V3 dv;
-				if constexpr (kStage) {
-					dv = hs.get(2);
-				} else {
-					const auto& cur = *uniform_ptr(opaque(levels) + level);
-					dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
-				}
+				const auto& cur = *uniform_ptr(opaque(levels) + level);
+				const V3 dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
 				zero = -dot4z(dv, R) <= 0.0;
 			}
 			// the reference's castRay still maps the ray into every object space (may raise)
@@ -613,14 +568,7 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	// terms of k_shade from the verdicts in registers
 	if (kPacket && B.fused && on) {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
-		V3 dv;
-		if constexpr (kStage) {
-			P = hs.get(0);
-			N = hs.get(1);
-			dv = hs.get(2);
-		} else {
-			dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
-		}
+		const V3 dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
 		shade_hit(S, cur, h, P, N, dv, [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
 		          glibc_pow_data::kLogTab, glibc_pow_data::kExpTab, ctr);
 	}
@@ -635,13 +583,11 @@ __global__ void __launch_bounds__(kBlock)
                                                                      unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
-	__shared__ double hit_lds[(kPacket && RT_HIT_LDS) ? 9 * kBlock : 1];
 	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
-	if constexpr (!kPacket) load_treelet(S);
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
-		shadow_item<kPacket, kCount>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds, hit_lds);
+		shadow_item<kPacket, kCount>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -803,8 +749,6 @@ __global__ void k_selftest(int op, const double* x, const double* y, double* out
 		out[i] = sqrt(x[i]);
 	} else if (op == 2) {
 		out[i] = x[i] / y[i];
-	} else if (op == 3) {  // the shared-divisor quotient of test_face (intersect.h qdiv)
-		out[i] = qdiv(x[i], recip(y[i]));
 	} else if (op == 4) {  // normalized3 of the vector (x[i], y[i], x[i + n]) (component x; .y, .z below)
 		out[i] = normalized3(mk(x[i], y[i], x[(i + n / 2) % n])).x;
 	} else if (op == 5) {

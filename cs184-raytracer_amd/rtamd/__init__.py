@@ -470,9 +470,8 @@ def device_count() -> int:
 
 def selftest_math(op: str, x: np.ndarray, y: Optional[np.ndarray] = None, device: int = 0) -> np.ndarray:
     """Runs the kernels' device pow/sqrt/div on the GPU for comparison with the host libm.
-    "qdiv": x / y by the shared-divisor sequence (intersect.h qdiv); "norm_x|y|z": component of
-    normalized3 of the vector (x[i], y[i], x[(i + n/2) % n])."""
-    code = {"pow": 0, "sqrt": 1, "div": 2, "qdiv": 3, "norm_x": 4, "norm_y": 5, "norm_z": 6}[op]
+    "norm_x|y|z": component of normalized3 of the vector (x[i], y[i], x[(i + n/2) % n])."""
+    code = {"pow": 0, "sqrt": 1, "div": 2, "norm_x": 4, "norm_y": 5, "norm_z": 6}[op]
     x = np.ascontiguousarray(x, dtype=np.float64)
     yy = np.ascontiguousarray(y if y is not None else x, dtype=np.float64)
     out = np.empty_like(x)
