@@ -43,7 +43,10 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "cs184-raytracer_amd"))
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md, memory hierarchy)
-L2_PEAK_GBS = 34500.0       # MI355X aggregate L2 bandwidth, 8 XCDs (MI355X_MICROARCH.md, L2)
+# L2-served gather rate of the whole chip: rows every workgroup shares, served from each XCD's
+# L2, measured 16.8-18.8 TB/s (MI355X_MICROARCH.md "Indexed rows: gather into LDS", the table's
+# first row); the upper figure is the roof (the scene's nodes and faces are such shared rows)
+L2_PEAK_GBS = 18800.0
 FP64_PEAK_TFLOPS = 78.6     # MI355X vector FP64
 NODE_BYTES, TRI_BYTES, NRM_BYTES = 64, 72, 72   # SURVEY.md §8d algorithmic bytes (64-B fp32-box node)
 RAY_IO_BYTES, PIXEL_BYTES = 64 + 64, 24
@@ -356,7 +359,8 @@ def roofline(solo, frames, traffic_path, concurrent, valu_path=None):
     roofs = {
         "l2": {"achieved": alg_bytes / t_launch_s / 1e9, "peak": L2_PEAK_GBS, "unit": "GB/s",
                "what": "SURVEY.md §8d algorithmic bytes (ray I/O + LBVH nodes + triangles + normals; the scene "
-                       "is L2/MALL-resident) / solo launch time vs the aggregate L2 bandwidth"},
+                       "is L2/MALL-resident) / solo launch time vs the chip's measured L2-served gather rate "
+                       "(18.8 TB/s, MI355X_MICROARCH.md 'Indexed rows: gather into LDS')"},
         "fp64": {"achieved": flops / t_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                  "what": "SURVEY.md §8d algorithmic FP64 flops / solo launch time vs vector FP64 peak"},
     }
@@ -534,6 +538,33 @@ def strong_scaling(a, world, rank, local, groups, dist, torch):
     return out
 
 
+def rank_topology(a, world, rank, local, dist, torch):
+    """Which GPU every rank drives, so that a multi-GPU line proves itself: the PCI address of
+    each rank's device, gathered to every rank, and the RCCL communicator's size.  Over RCCL
+    (backend nccl) two ranks on one GPU make the scaling figures meaningless: the run stops
+    with exit code 3 before any timing (gloo rehearsals may share a GPU on purpose)."""
+    p = torch.cuda.get_device_properties(local)
+    me = "%04x:%02x:%02x" % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    if world > 1:
+        ids = [None] * world
+        with stdout_to_stderr():
+            grp = dist.new_group(backend="gloo")  # host-side exchange: no RCCL communicator yet
+            dist.all_gather_object(ids, me, group=grp)
+            dist.destroy_process_group(grp)
+    else:
+        ids = [me]
+    nccl = world > 1 and dist.get_backend() == "nccl"
+    topo = {"backend": dist.get_backend() if world > 1 else None, "world_size": world,
+            "rccl_nranks": world if nccl else None, "rank_pci_bus_ids": ids,
+            "distinct_gpus": len(set(ids))}
+    if nccl and len(set(ids)) != world:
+        if rank == 0:
+            sys.stderr.write("bench.py: %d RCCL ranks drive only %d distinct GPUs (%s): every rank needs a GPU of its "
+                             "own for a scaling measurement\n" % (world, len(set(ids)), ", ".join(ids)))
+        sys.exit(3)
+    return topo
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", 0))
@@ -550,11 +581,13 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         with stdout_to_stderr():
-            if a.backend == "nccl":
-                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-            else:
-                dist.init_process_group("gloo")
-            dist.barrier()  # the connections are made (and reported) here
+            # nccl without device_id: its communicator is made at the first collective, after
+            # rank_topology has checked that every rank drives a GPU of its own
+            dist.init_process_group(a.backend)
+    topology = rank_topology(a, world, rank, local, dist, torch)
+    if world > 1:
+        with stdout_to_stderr():
+            dist.barrier(device_ids=[local] if a.backend == "nccl" else None)  # the connections are made here
     scene_rel, W, H, flags = CONFIGS[a.config]
     kw = option_kwargs(flags)
     scene = os.path.join(SCENES, scene_rel)
@@ -734,6 +767,7 @@ def main():
             "work_per_frame_rank0": work,
             "traversal_work_per_frame": solo["work_per_frame"] if solo else None,
             "strong_scaling": sweep,
+            "topology": topology,
         }
         if res["roofline"]:
             # the dominant kernel's solo time per step must fit in the step (a consistent time base)

@@ -28,6 +28,11 @@ int fail(int code, const std::string& msg) {
 	return code;
 }
 
+double now_s() {
+	using clk = std::chrono::steady_clock;
+	return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
+}
+
 #define HIP_TRY(expr)                                                                         \
 	do {                                                                                      \
 		hipError_t e_ = (expr);                                                               \
@@ -91,6 +96,7 @@ struct Progress {
 struct LevelBuffers {
 	rtamd::RayLevel lv{};
 	void* block = nullptr;
+	int64_t bytes = 0;
 };
 
 // A chunk shape traced once host-driven becomes a plan: the same launch sequence with every
@@ -173,6 +179,8 @@ struct Lane {
 	// buffer is reallocated
 	std::vector<Plan> plans;
 	const Plan* planned = nullptr;        // the plan replaying the current chunk, if any
+	bool forked = false;                  // this call's caller stream joined into the lane's streams
+	bool direct = false;                  // the current chunk runs on the caller's stream (Render::start_chunk)
 };
 
 void clear_plans(Lane& ln) {
@@ -243,6 +251,15 @@ struct rt_scene {
 	// stream (Render::issue_plan)
 	int64_t one_stream_pixels = (int64_t)1 << 17;
 	int one_stream_level1 = 1;  // RTAMD_ONE_STREAM_LEVEL1: a plan of one traced level on one stream too
+	// RTAMD_FUSED: a replayed one-stream chunk traces every level in ONE launch (k_fused: closest
+	// hits + shadow rays + Phong terms, and for a plan of one level the output pixels too)
+	// instead of k_closest + k_shadow (+ k_shade) per level and k_output
+	int fused = 1;
+	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
+	// (no fork/join across queues) and its last kernel finishes the statistics (no
+	// k_stats_finish launch)
+	int direct = 1;
+	uint32_t* fin_done = nullptr;  // device: blocks done of a launch that finishes the statistics
 	int all_lights_for(int first_level, int64_t hits, int64_t light_major_below) const {
 		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
 		if (al && ds.n_nonambient > 1 && hits < light_major_below) al = 0;
@@ -285,6 +302,8 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		HIP_TRY(hipDeviceSynchronize());
 		HIP_TRY(hipFree(L.block));
 		L.block = nullptr;
+		s->info.level_bytes -= L.bytes;
+		L.bytes = 0;
 	}
 	capacity = std::max<int64_t>(capacity, 1024);
 	const int64_t n = capacity;
@@ -294,6 +313,8 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
 	const int64_t bytes = 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
 	HIP_TRY(hipMalloc(&L.block, bytes));
+	L.bytes = bytes;
+	s->info.level_bytes += bytes;
 	char* p = static_cast<char*>(L.block);
 	auto take = [&](int64_t b) {
 		char* r = p;
@@ -410,6 +431,33 @@ struct Render {
 	rt_counters cnt{};
 	float kernel_ms = 0.f;
 	Progress* progress = nullptr;
+	hipStream_t caller = nullptr;
+	bool fork_recorded = false;
+	bool direct_ok = false;    // the call is one chunk on one lane: it may run on the caller's stream
+	bool stats_fused = false;  // the call's last kernel finishes the statistics (no k_stats_finish)
+	bool finished = false;     // the plan issued last attached the statistics finish to a launch
+	static constexpr int64_t kFinishBlocks = 2048;
+
+	// the caller's prior work before any of this lane's (the fork), once per call; a chunk
+	// on the caller's own stream needs none
+	int fork(Lane& ln) {
+		if (ln.forked) return RT_OK;
+		if (!fork_recorded) HIP_TRY(hipEventRecord(s->fork_event, caller));
+		fork_recorded = true;
+		HIP_TRY(hipStreamWaitEvent(ln.stream, s->fork_event, 0));
+		ln.forked = true;
+		return RT_OK;
+	}
+
+	// a replayed chunk of this plan is issued on one stream (issue_plan)
+	bool one_stream(const Lane& ln, const Plan& pl) const {
+		return ln.n0 <= s->one_stream_pixels || (pl.n_levels == 1 && s->one_stream_level1);
+	}
+	// its levels are fused launches (k_fused): shaded renders of at most 64 shadow lights,
+	// without the work counters
+	bool fusable(const Lane& ln) const {
+		return s->fused && !ln.io && !s->ds.work_stats && s->ds.n_nonambient <= rtamd::kMaxShadowLights;
+	}
 
 	// k_closest of level L, then the read-back of its counts.  n: the level's ray count, or
 	// with n_dev (the previous level's child counter) an upper bound: the level is queued
@@ -536,7 +584,7 @@ struct Render {
 	// as soon as their k_closest is done, the deep levels in batches on shade[3] after the
 	// chain, then reductions and the output.  capture: recorded into a graph (with events
 	// of its own; the row table it reads is rewritten for every chunk).
-	int issue_plan(Lane& ln, Plan& pl, bool capture) {
+	int issue_plan(Lane& ln, Plan& pl, bool capture, hipStream_t st, bool finish) {
 		const int nlev = pl.n_levels, depth = ln.depth;
 		int rc = RT_OK;
 		std::vector<hipEvent_t> tmp;
@@ -554,7 +602,6 @@ struct Render {
 			if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string("planned launch: ") + hipGetErrorString(e));
 		};
 		int launches[3] = {0, 0, 0};
-		hipStream_t st = ln.stream;
 		std::vector<hipEvent_t> joins;
 		Plan scratch = pl;
 		// A small chunk (a small frame, or a GPU's row share of one) is issued on ONE stream:
@@ -564,7 +611,48 @@ struct Render {
 		// A plan of one traced level (no bounce: bdepth 0, or nothing reflective was hit) has
 		// nothing to overlap either: C2a 0.185 -> 0.179, C2b 0.334 -> 0.327, C4 0.357 -> 0.355 ms,
 		// C4 2-way share 0.302 -> 0.290 ms (RTAMD_ONE_STREAM_LEVEL1)
-		if (ln.n0 <= s->one_stream_pixels || (nlev == 1 && s->one_stream_level1)) {
+		// the statistics finish inside the last launch (finish: a call of this one chunk), where
+		// that launch has at most kFinishBlocks blocks: every block counts itself done on one
+		// device-scope counter, which takes ~88 atomics per us (MI355X_MICROARCH.md "dequeue");
+		// a larger grid leaves the finish to k_stats_finish on the same stream
+		rtamd::FusedOut fin{};
+		fin.summary = s->summary_mapped;
+		fin.done = s->fin_done;
+		finished = false;
+		auto finish_on = [&](int64_t threads, int block) {
+			const bool on = finish && (threads + block - 1) / block <= kFinishBlocks;
+			finished = finished || on;
+			return on;
+		};
+		const int64_t tiles = ((ln.fg.width + 7) / 8) * ((ln.n0 / ln.fg.width + 7) / 8) * 64;  // level-0 packet threads
+		if (one_stream(ln, pl) && fusable(ln)) {
+			// every level in one launch (k_fused), level after level; a plan of one level writes
+			// the pixels from there, else the reductions and k_output follow
+			for (int L = 0; L < nlev && rc == RT_OK; L++) {
+				const int remaining = depth - L;
+				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
+				rtamd::FusedOut fo{};
+				if (nlev == 1) {
+					fo = finish_on((s->packet_mask & rtamd::kPacketClosest0) ? tiles : ln.n0, 128) ? fin : rtamd::FusedOut{};
+					fo.final = 1;
+				}
+				step(rtamd::launch_fused(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
+				                         remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
+				                         L == nlev - 1 && remaining > 0, fo));
+				launches[0]++;
+			}
+			if (nlev > 1) {
+				for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
+					step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1,
+					                                ln.levels[l].lv, ln.levels[l + 1].lv, st));
+				if (rc == RT_OK)
+					step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, &ln.levels[1].lv, s->stats, st, s->ctr,
+					                          finish_on(ln.n0, 256) ? &fin : nullptr));
+			}
+			for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
+			return rc;
+		}
+		if (one_stream(ln, pl)) {
 			for (int L = 0; L < nlev && rc == RT_OK; L++) {
 				const int remaining = depth - L;
 				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
@@ -632,7 +720,7 @@ struct Render {
 			                                ln.levels[l + 1].lv, st));
 		if (rc == RT_OK)
 			step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
-			                          st));
+			                          st, s->ctr, finish_on(ln.n0, 256) ? &fin : nullptr));
 		for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
 		for (hipEvent_t e : tmp) (void)hipEventDestroy(e);
 		return rc;
@@ -651,7 +739,7 @@ struct Render {
 		if (s->graphs == 1) {
 			hipGraph_t graph = nullptr;
 			HIP_TRY(hipStreamBeginCapture(ln.stream, hipStreamCaptureModeThreadLocal));
-			int rc = issue_plan(ln, pl, true);
+			int rc = issue_plan(ln, pl, true, ln.stream, false);
 			const hipError_t ec = hipStreamEndCapture(ln.stream, &graph);
 			if (rc == RT_OK && ec != hipSuccess)
 				rc = fail(RT_ERR_DEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
@@ -696,8 +784,10 @@ struct Render {
 		return nullptr;
 	}
 
-	// the chunk's row table: image row and output rows of every selected row of its pieces
-	int upload_rows(Lane& ln, const std::vector<Segment>& segs, int64_t n_rows) {
+	// the chunk's row table: image row and output rows of every selected row of its pieces,
+	// staged in pinned memory (and hashed for the plan key); *copy: it differs from the table
+	// now on the device (copy_rows, on the stream the chunk runs on)
+	int prepare_rows(Lane& ln, const std::vector<Segment>& segs, int64_t n_rows, bool* copy) {
 		if (ln.rows_cap < n_rows) {
 			clear_plans(ln);  // graphs hold the table's address
 			if (ln.rows_dev) HIP_TRY(hipFree(ln.rows_dev));
@@ -735,9 +825,7 @@ struct Render {
 			}
 		}
 		ln.rows_hash = h;
-		if (!same)
-			HIP_TRY(hipMemcpyAsync(ln.rows_dev, ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow), hipMemcpyHostToDevice,
-			                       ln.stream));
+		*copy = !same;
 		ln.rows_uploaded = n_rows;
 		return RT_OK;
 	}
@@ -751,7 +839,8 @@ struct Render {
 		ln.depth = first.depth;
 		ln.io = first.io;
 		ln.n0 = n_rows * first.W;
-		int rc = upload_rows(ln, segs, n_rows);
+		bool copy_rows = false;
+		int rc = prepare_rows(ln, segs, n_rows, &copy_rows);
 		if (rc) return rc;
 		ln.fg = rtamd::FrameGeometry{};
 		ln.fg.width = first.p->width;
@@ -764,15 +853,25 @@ struct Render {
 		ln.deferred.clear();
 		ln.planned = nullptr;
 		Plan* pl = find_plan(ln, key_of(ln));
+		// the call's only chunk, replaying a plan of this lane's own on one stream: it runs on
+		// the caller's stream (no fork, no join); otherwise on the lane's streams after the fork
+		ln.direct = s->direct && direct_ok && pl && !pl->exec && one_stream(ln, *pl);
+		const hipStream_t st = ln.direct ? caller : ln.stream;
+		if (!ln.direct && (rc = fork(ln))) return rc;
+		if (copy_rows)
+			HIP_TRY(hipMemcpyAsync(ln.rows_dev, ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow), hipMemcpyHostToDevice, st));
 		if (!pl && (pl = adopt_plan(ln, key_of(ln), rc), rc)) return rc;
 		if (pl) {
 			if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
+			// the call's only chunk finishes the statistics in its last kernel (pinned summary)
+			const bool finish = direct_ok && !pl->exec && s->summary_mapped;
 			if (pl->exec) {
-				HIP_TRY(hipGraphLaunch(pl->exec, ln.stream));
-			} else if ((rc = issue_plan(ln, *pl, false))) {
+				HIP_TRY(hipGraphLaunch(pl->exec, st));
+			} else if ((rc = issue_plan(ln, *pl, false, st, finish))) {
 				return rc;
 			}
-			HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
+			stats_fused = stats_fused || (finish && finished);
+			HIP_TRY(hipEventRecord(ln.chunk_done, st));
 			ln.planned = pl;
 			ln.phase = Lane::FINISHING;
 			return RT_OK;
@@ -1117,7 +1216,9 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 		return fail(RT_ERR_DEVICE, "no HIP device available (the rtamd render path runs only on the GPU)");
 	if (device < 0 || device >= ndev) return fail(RT_ERR_ARG, "bad device index");
 	HIP_TRY(hipSetDevice(device));
+	const double t_build = now_s();
 	rtamd::FlatScene fs = rtamd::flatten_scene(scene);
+	const double t_upload = now_s();
 	std::unique_ptr<rt_scene> s(new rt_scene());
 	s->device = device;
 	// tuning knobs; lanes are created on first use
@@ -1134,6 +1235,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 		s->light_major_below_single = s->light_major_below_batch = std::atoll(lm);
 	if (const char* os = std::getenv("RTAMD_ONE_STREAM_PIXELS")) s->one_stream_pixels = std::atoll(os);
 	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
+	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
+	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
 	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);
@@ -1165,6 +1268,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	}
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_may_raise = fs.n_may_raise;
+	for (const auto& g : fs.geoms) s->ds.n_meshes += g.kind == rtamd::DGEOM_MESH ? 1 : 0;
 	if (const char* ws = std::getenv("RTAMD_WORK_STATS")) s->force_work_stats = std::atoi(ws) != 0;
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	// j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
@@ -1184,6 +1288,11 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	HIP_TRY(hipMalloc(&st, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
 	s->allocs.push_back(st);
 	s->stats = static_cast<unsigned long long*>(st);
+	void* fd = nullptr;
+	HIP_TRY(hipMalloc(&fd, 64));
+	s->allocs.push_back(fd);
+	s->fin_done = static_cast<uint32_t*>(fd);
+	HIP_TRY(hipMemset(s->fin_done, 0, 64));
 	void* sm = nullptr;
 	HIP_TRY(hipMalloc(&sm, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1)));
 	s->allocs.push_back(sm);
@@ -1206,6 +1315,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	in.n_faces = static_cast<int64_t>(fs.face_geo.size());
 	in.n_bvh_nodes = static_cast<int64_t>(fs.nodes.size());
 	in.max_bvh_depth = fs.max_bvh_depth;
+	in.build_ms = (t_upload - t_build) * 1e3;
+	in.upload_ms = (now_s() - t_upload) * 1e3;
 	*out = s.release();
 	return RT_OK;
 }
@@ -1237,10 +1348,6 @@ namespace {
 // lanes the chunks (of one image, or whole images of a batch) are traced concurrently
 // and one image's latency-bound deep levels overlap another's wide first levels.
 // --intersection-only jobs come one per call (their maximum is a per-image statistic).
-double now_s() {
-	using clk = std::chrono::steady_clock;
-	return std::chrono::duration<double>(clk::now().time_since_epoch()).count();
-}
 
 // After a failed render: nothing of it may outlive the call.  Queued kernels finish (they
 // may still write the caller's buffers, which the caller must not free before this
@@ -1261,6 +1368,7 @@ void reset_after_error(rt_scene* s) {
 	}
 	(void)hipMemset(s->stats, 0, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride);
 	(void)hipMemset(s->ctr, 0, sizeof(rtamd::DeviceCounters));
+	(void)hipMemset(s->fin_done, 0, 64);
 	(void)hipDeviceSynchronize();
 	(void)hipGetLastError();
 }
@@ -1399,6 +1507,16 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 		const int64_t max_rows = std::max<int64_t>(1, limit / std::max<int64_t>(1, j.W));
 		const int64_t pieces = (j.n_rows + max_rows - 1) / max_rows;
 		n_lanes = pieces > 1 ? 2 : 1;
+		// each lane keeps level buffers of its own (~200 B per ray of a 4 M-pixel chunk per
+		// level, kept after the render): a second lane only while free HBM holds it four times
+		// over (C5, 4096^2 at depth 8: rt_scene_info.level_bytes)
+		if (n_lanes == 2 && s->lanes.size() < 2) {
+			size_t free_b = 0, total_b = 0;
+			const double lane_bytes = 200.0 * static_cast<double>(std::min<int64_t>(limit, j.n_rows * j.W)) *
+			                          std::min(j.depth + 1, 8);
+			if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && static_cast<double>(free_b) < 4 * lane_bytes)
+				n_lanes = 1;
+		}
 		chunks_per_lane = static_cast<int>(std::max<int64_t>(1, (pieces + 1) / 2));
 	}
 	int rc = ensure_lanes(s, n_lanes);
@@ -1410,11 +1528,13 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	R.progress = progress;
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
 	// the caller's stream is joined first (its prior work, e.g. the allocation of the
-	// output buffers, completes before ours starts); the call returns when all is done
-	HIP_TRY(hipEventRecord(s->fork_event, caller));
-	for (size_t k = 0; k < n_lanes; k++) HIP_TRY(hipStreamWaitEvent(s->lanes[k]->stream, s->fork_event, 0));
+	// output buffers, completes before ours starts: Render::fork, as a lane starts its first
+	// chunk); the call returns when all is done
+	R.caller = caller;
+	for (size_t k = 0; k < n_lanes; k++) s->lanes[k]->forked = false;
 	const std::vector<std::vector<Segment>> chunks =
 	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, s->batch_balance, chunks_per_lane);
+	R.direct_ok = n_lanes == 1 && chunks.size() == 1;
 	size_t next_chunk = 0;
 	std::unique_ptr<rtamd::MarkerRange> trace_range(new rtamd::MarkerRange("rtamd: trace (levels, shading, output)"));
 	// The statistics reduction is queued on the caller's stream, behind every lane's last
@@ -1423,7 +1543,10 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	// small frame (profiles/round3 marker trace)
 	bool stats_issued = false;
 	auto issue_stats = [&]() -> int {
-		for (size_t k = 0; k < n_lanes; k++) HIP_TRY(hipStreamWaitEvent(caller, s->lanes[k]->chunk_done, 0));
+		stats_issued = true;
+		if (R.stats_fused) return RT_OK;  // done by the call's last kernel (k_fused / k_output)
+		for (size_t k = 0; k < n_lanes; k++)
+			if (s->lanes[k]->forked) HIP_TRY(hipStreamWaitEvent(caller, s->lanes[k]->chunk_done, 0));
 		if (s->summary_mapped) {
 			HIP_TRY(rtamd::launch_stats_finish(s->stats, s->ctr, s->summary_mapped, caller));
 		} else {
@@ -1614,6 +1737,7 @@ bool whole_image(const rt_render_params* p) { return p->row_begin == 0 && p->row
 
 int render_batch(rt_scene* s, int n, const rt_render_params* params, double* const* out_rgb_dev,
                  uint8_t* const* out_rgb8_dev, void* stream_v, rt_counters* counters, Progress* progress) {
+	const double t0 = now_s();
 	if (!s || !params || n < 0) return fail(RT_ERR_ARG, "null scene or params");
 	for (int k = 0; k < n; k++) {
 		const int rc = check_params(s, params + k);
@@ -1658,6 +1782,7 @@ int render_batch(rt_scene* s, int n, const rt_render_params* params, double* con
 	}
 	const int rc = flush();
 	if (rc) return rc;
+	total.host_ms = (now_s() - t0) * 1e3;
 	if (counters) *counters = total;
 	return RT_OK;
 }
@@ -1682,11 +1807,17 @@ int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint
 	if (progress) progress(0, pr.total, user);
 	double* rgb_dev = (out_rgb || p->intersection_only) ? s->out_dev : nullptr;
 	uint8_t* rgb8_dev = out_rgb8 ? s->out8_dev : nullptr;
+	const double t0 = now_s();
 	rc = render_batch(s, 1, p, &rgb_dev, &rgb8_dev, nullptr, counters, &pr);
 	if (rc) return rc;
 	rtamd::MarkerRange cr("rtamd: image to host (PCIe)");
+	const double t_copy = now_s();
 	if (out_rgb) HIP_TRY(hipMemcpy(out_rgb, s->out_dev, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
 	if (out_rgb8) HIP_TRY(hipMemcpy(out_rgb8, s->out8_dev, n * 3, hipMemcpyDeviceToHost));
+	if (counters) {
+		counters->copy_ms = (now_s() - t_copy) * 1e3;
+		counters->host_ms = (now_s() - t0) * 1e3;
+	}
 	if (progress) progress(pr.total, pr.total, user);
 	return RT_OK;
 }

@@ -5,11 +5,14 @@
 // --gpus N (devices --device .. --device+N-1 of this node, rows in --row-block blocks
 // interleaved over them, gathered over RCCL: include/rtamd_multi.h) and --devices LIST
 // (an explicit comma-separated device list for that path; a repeated device makes
-// partitions sharing one GPU).
+// partitions sharing one GPU).  --timing FILE writes the host time of every phase of the run
+// as JSON (HIP runtime start, parse, LBVH build, HBM upload, render, device-to-host copy,
+// PNG): the drop-in's wall-clock split (tools/cli_bench.py).
 // The render itself runs on the GPU through the C-ABI (include/rtamd.h).
 #include <getopt.h>
 #include <signal.h>
 #include <sys/time.h>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
@@ -25,14 +28,14 @@ namespace {
 
 struct Options {  // options.h:10-16 defaults
 	std::vector<std::string> inputs;
-	std::string output, dump_raw;
+	std::string output, dump_raw, timing;
 	int threads = 1, width = 500, height = 500, bdepth = 10, device = 0;
 	int gpus = 0, row_block = 8;  // gpus 0: the single-device path
 	std::vector<int> devices;     // --devices: explicit list for the multi-device path
 	bool intersection_only = false;
 };
 
-enum { OPT_HELP = 0, OPT_BDEPTH = 256, OPT_IO, OPT_DEVICE, OPT_DUMP, OPT_GPUS, OPT_ROW_BLOCK, OPT_DEVICES };
+enum { OPT_HELP = 0, OPT_BDEPTH = 256, OPT_IO, OPT_DEVICE, OPT_DUMP, OPT_GPUS, OPT_ROW_BLOCK, OPT_DEVICES, OPT_TIMING };
 
 bool parse_int(const char* s, int& out) {
 	try {
@@ -50,13 +53,15 @@ bool parse_command_line(int argc, char** argv, Options& o) {  // options.cpp:18-
 	                                     {"intersection-only", 0, nullptr, OPT_IO},
 	                                     {"device", 1, nullptr, OPT_DEVICE}, {"dump-raw", 1, nullptr, OPT_DUMP},
 	                                     {"gpus", 1, nullptr, OPT_GPUS},     {"row-block", 1, nullptr, OPT_ROW_BLOCK},
-	                                     {"devices", 1, nullptr, OPT_DEVICES}, {nullptr, 0, nullptr, 0}};
+	                                     {"devices", 1, nullptr, OPT_DEVICES}, {"timing", 1, nullptr, OPT_TIMING},
+	                                     {nullptr, 0, nullptr, 0}};
 	int c;
 	while ((c = getopt_long(argc, argv, "t:w:h:o:", opts, nullptr)) != -1) {
 		switch (c) {
 			case 'o': o.output = optarg; break;
 			case OPT_IO: o.intersection_only = true; break;
 			case OPT_DUMP: o.dump_raw = optarg; break;
+			case OPT_TIMING: o.timing = optarg; break;
 			case 't':
 				if (!parse_int(optarg, o.threads)) {
 					std::cerr << "Error: Thread count is invalid." << std::endl;
@@ -160,9 +165,34 @@ void update_progress(int complete, int total, void*) {  // main.cpp:12-22
 	g_progress_signaled = 0;
 }
 
+double now_ms() {
+	using clk = std::chrono::steady_clock;
+	return std::chrono::duration<double, std::milli>(clk::now().time_since_epoch()).count();
+}
+
+// host milliseconds of the run's phases (--timing)
+struct Timing {
+	double start = now_ms(), last = start;
+	std::vector<std::pair<std::string, double>> phases;
+	void mark(const char* name) {
+		const double t = now_ms();
+		phases.emplace_back(name, t - last);
+		last = t;
+	}
+	void write(const std::string& path) const {
+		FILE* f = std::fopen(path.c_str(), "w");
+		if (!f) return;
+		std::fprintf(f, "{");
+		for (const auto& p : phases) std::fprintf(f, "\"%s_ms\": %.3f, ", p.first.c_str(), p.second);
+		std::fprintf(f, "\"main_ms\": %.3f}\n", last - start);
+		std::fclose(f);
+	}
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
+	Timing tm;
 	Options o;
 	if (!parse_command_line(argc, argv, o)) return 1;
 	if (!std::ofstream(o.output)) {  // main.cpp:45-51
@@ -170,6 +200,10 @@ int main(int argc, char** argv) {
 		return 1;
 	}
 	std::remove(o.output.c_str());
+	if (!o.timing.empty()) {
+		(void)rt_device_count();  // starts the HIP runtime (otherwise inside rt_scene_create)
+		tm.mark("hip_init");
+	}
 	rt_builder* b = rt_builder_create();
 	for (const std::string& f : o.inputs) {
 		const int rc = rt_builder_parse_rti(b, f.c_str());
@@ -188,6 +222,7 @@ int main(int argc, char** argv) {
 		std::cerr << "Error: At least one camera must be specified." << std::endl;
 		return 1;
 	}
+	tm.mark("parse");
 	rt_scene* scene = nullptr;
 	rt_multi* multi = nullptr;
 	if (o.gpus > 0) {
@@ -202,6 +237,13 @@ int main(int argc, char** argv) {
 		std::cerr << "Error: " << rt_last_error() << std::endl;
 		return 1;
 	}
+	if (scene) {
+		rt_scene_info info{};
+		rt_scene_get_info(scene, &info);
+		tm.phases.emplace_back("scene_build", info.build_ms);
+		tm.phases.emplace_back("scene_upload", info.upload_ms);
+	}
+	tm.mark("scene_create");
 	rt_render_params p{};
 	p.width = o.width;
 	p.height = o.height;
@@ -216,11 +258,17 @@ int main(int argc, char** argv) {
 	std::vector<double> img(o.dump_raw.empty() ? 0 : n);
 	std::vector<uint8_t> rgb(n);
 	set_alarm(true);
+	rt_counters cnt{};
 	int rc = multi ? rt_multi_render(multi, &p, img.empty() ? nullptr : img.data(), rgb.data(), update_progress,
 	                                 nullptr, nullptr)
-	         : img.empty() ? rt_render_rgb8(scene, &p, rgb.data(), update_progress, nullptr, nullptr)
-	                       : rt_render(scene, &p, img.data(), update_progress, nullptr, nullptr);
+	         : img.empty() ? rt_render_rgb8(scene, &p, rgb.data(), update_progress, nullptr, &cnt)
+	                       : rt_render(scene, &p, img.data(), update_progress, nullptr, &cnt);
 	set_alarm(false);
+	if (scene) {
+		tm.phases.emplace_back("render_gpu", cnt.host_ms - cnt.copy_ms);
+		tm.phases.emplace_back("d2h", cnt.copy_ms);
+	}
+	tm.mark("render");
 	if (rc == RT_ERR_MATH) {
 		std::cerr << "terminate called after throwing an instance of 'MathException'\n  what():  " << rt_last_error()
 		          << std::endl;
@@ -242,8 +290,11 @@ int main(int argc, char** argv) {
 		std::cerr << "Error: " << rt_last_error() << std::endl;
 		return 1;
 	}
+	tm.mark("png");
 	if (scene) rt_scene_destroy(scene);
 	if (multi) rt_multi_destroy(multi);
 	rt_builder_destroy(b);
+	tm.mark("teardown");
+	if (!o.timing.empty()) tm.write(o.timing);
 	return 0;
 }

@@ -633,18 +633,20 @@ __device__ __forceinline__ V3 face_point(const DeviceScene& S, const FaceHit& h)
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	return mk(p0.x + (h.a * va.x + h.b * vb.x), p0.y + (h.a * va.y + h.b * vb.y), p0.z + (h.a * va.z + h.b * vb.z));
 }
+template <bool kMesh>
 __device__ __forceinline__ V3 hit_point(const DeviceScene& S, const FaceHit& h, V3 oo, V3 dd) {
-	return h.face < 0 ? oo + h.a * dd : face_point(S, h);
+	return (!kMesh || h.face < 0) ? oo + h.a * dd : face_point(S, h);
 }
 
 // The closest-hit searches keep only (geometry, face, a, b) of the best hit so far; its
 // world point and object-space normal are recomputed once at the end with the same
 // expressions (bit-identical, fewer live registers during the traversals).
+template <bool kMesh>
 __device__ __forceinline__ void winner_point_normal(const DeviceScene& S, int g, const FaceHit& h, V3 o, V3 d,
                                                     V3& Pw, V3& No) {
 	const DGeom* G = S.geoms + g;
 	V3 Po;
-	if (h.face < 0) {
+	if (!kMesh || h.face < 0) {
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		Po = oo + h.a * normalized3(draw);
@@ -672,7 +674,9 @@ __device__ __forceinline__ void check_may_raise(const DeviceScene& S, V3 d, bool
 // insertion order.  A geometry whose padded world box the ray misses, or enters beyond
 // the current best distance, cannot be the answer and is skipped without its
 // object-space transform.
-template <typename WS>
+// kMesh false: a scene of spheres only (DeviceScene::n_meshes == 0), instantiated without
+// the mesh search (fewer registers for the sphere loop: DESIGN.md §4)
+template <bool kMesh, typename WS>
 __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, double& best_dist, int& best_geom, V3& hitP,
                             V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WS& ws) {
 	bool found = false;
@@ -693,16 +697,19 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 		FaceHit h{-1, 0, 0};
 		bool hit, settled;
 		double fd;
-		if (G->kind == DGEOM_SPHERE) {
+		V3 Pw;
+		if (!kMesh || G->kind == DGEOM_SPHERE) {
 			ws.inc(W_SPHERES);
 			PROF_BEGIN(ts);
 			hit = sphere_hit(G, oo, dd, reverse, h.a);
-		PROF_END(ws, PH_SPHERE, ts);
+			PROF_END(ws, PH_SPHERE, ts);
+			if (!hit) continue;
+			Pw = xf_point(G->fwd, oo + h.a * dd);
 		} else {
 			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
+			if (!hit) continue;
+			Pw = xf_point(G->fwd, face_point(S, h));  // a mesh hit is a face (geometry.cpp:121)
 		}
-		if (!hit) continue;
-		const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
 		const double dist = sqrt(sq4(Pw - o));
 		if (found && dist >= best_dist) continue;
 		found = true;
@@ -710,7 +717,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 		best_geom = g;
 		best = h;
 	}
-	if (found) winner_point_normal(S, best_geom, best, o, d, hitP, hitNobj);
+	if (found) winner_point_normal<kMesh>(S, best_geom, best, o, d, hitP, hitNobj);
 	return found;
 }
 
@@ -721,7 +728,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 // face up to slightly beyond it means no occlusion.  Only a closest face within a
 // relative 1e-7 of the light distance falls back to the reference's full comparison.
 // geom_occludes: geometry G (its world box already passed) occludes the shadow ray.
-template <typename GP, typename WS>
+template <bool kMesh, typename GP, typename WS>
 __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double dist_light,
                               int32_t* stack, DeviceCounters* ctr, WS& ws) {
 	const bool inf_light = dist_light == INFINITY;
@@ -735,7 +742,7 @@ __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool rever
 	FaceHit h{-1, 0, 0};
 	bool hit, settled = false;
 	double fd;
-	if (G->kind == DGEOM_SPHERE) {
+	if (!kMesh || G->kind == DGEOM_SPHERE) {
 		ws.inc(W_SPHERES);
 		PROF_BEGIN(ts);
 		hit = sphere_hit(G, oo, dd, reverse, h.a);
@@ -757,7 +764,7 @@ __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool rever
 	}
 	if (!hit) return false;
 	if (inf_light || settled) return true;
-	const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
+	const V3 Pw = xf_point(G->fwd, hit_point<kMesh>(S, h, oo, dd));
 	return sqrt(sq4(Pw - o)) <= dist_light;
 }
 
@@ -766,7 +773,7 @@ __device__ __forceinline__ double shadow_slab_limit(double dist_light) {
 }
 
 // The `any` over the geometries, cheap ones first (DeviceScene::shadow_order).
-template <typename WS>
+template <bool kMesh, typename WS>
 __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, int32_t* stack,
                          DeviceCounters* ctr, WS& ws) {
 	const V3 winv = safe_inv(d);
@@ -778,7 +785,7 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 		PROF_BEGIN(tw0);
 		const bool wb = world_cull(G, o, winv, lim);
 		PROF_END(ws, PH_WORLD, tw0);
-		if (wb && geom_occludes(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
+		if (wb && geom_occludes<kMesh>(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
 	}
 	return false;
 }
@@ -915,7 +922,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	return true;
 }
 
-template <typename WS>
+template <bool kMesh, typename WS>
 __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, bool on, double& best_dist,
                                    int& best_geom, V3& hitP, V3& hitNobj, int32_t* wstack, DeviceCounters* ctr,
                                    WS& ws) {
@@ -938,7 +945,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 		FaceHit h{-1, 0, 0};
 		bool hit, settled;
 		double fd;
-		if (G->kind == DGEOM_SPHERE) {
+		if (!kMesh || G->kind == DGEOM_SPHERE) {
 			ws.add(W_SPHERES, cand);
 			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
@@ -947,7 +954,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 			hit = mesh_hit_packet<false>(S, G, oo, dd, reverse, cand, INFINITY, INFINITY, h, settled, fd, wstack, ws);
 		}
 		if (hit) {
-			const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
+			const V3 Pw = xf_point(G->fwd, hit_point<kMesh>(S, h, oo, dd));
 			const double dist = sqrt(sq4(Pw - o));
 			if (!(found && dist >= best_dist)) {
 				found = true;
@@ -957,12 +964,12 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 			}
 		}
 	}
-	if (found) winner_point_normal(S, best_geom, best, o, d, hitP, hitNobj);
+	if (found) winner_point_normal<kMesh>(S, best_geom, best, o, d, hitP, hitNobj);
 	return found;
 }
 
 // Packet form of occluded(): same decisions per lane (see occluded()).
-template <typename WS>
+template <bool kMesh, typename WS>
 __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, bool on,
                                 int32_t* wstack, DeviceCounters* ctr, WS& ws) {
 	const bool inf_light = dist_light == INFINITY;
@@ -990,7 +997,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		FaceHit h{-1, 0, 0};
 		bool hit, settled = false;
 		double fd = INFINITY;
-		if (G->kind == DGEOM_SPHERE) {
+		if (!kMesh || G->kind == DGEOM_SPHERE) {
 			ws.add(W_SPHERES, cand);
 			PROF_BEGIN(ts);
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
@@ -1019,7 +1026,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 			if (inf_light || settled) {
 				occ = true;
 			} else {
-				const V3 Pw = xf_point(G->fwd, hit_point(S, h, oo, dd));
+				const V3 Pw = xf_point(G->fwd, hit_point<kMesh>(S, h, oo, dd));
 				if (sqrt(sq4(Pw - o)) <= dist_light) occ = true;
 			}
 		}

@@ -224,6 +224,7 @@ int rt_multi_render(rt_multi* m, const rt_render_params* p, double* out_rgb, uin
 	for (std::thread& t : th) t.join();
 	for (int i = 0; i < n; i++)
 		if (rcs[i]) return fail(rcs[i], errs[i]);
+	phase.reset();  // the render range is popped before the next one is pushed (ranges nest)
 	phase.reset(new rtamd::MarkerRange("rtamd_multi: max all-reduce + row gather + assembly"));
 	const double tg = now_ms();
 	// 2. --intersection-only: the global maximum (scene.cpp:50-58), then normalise on every device

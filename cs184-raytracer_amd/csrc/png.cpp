@@ -11,11 +11,21 @@
 //   time, split into 8192-byte IDAT chunks                         pngwutil.c:295-420,1005-1135
 //   CMF window optimisation of the first IDAT for small images     pngwutil.c:251-288
 //   IEND
+// The filter choice of row y depends only on the raw rows y and y - 1, so the rows are
+// filtered in parallel (bands of rows handed out in order to host threads) while the calling
+// thread feeds the filtered rows to deflate in order, exactly as libpng does (one row per
+// deflate call, Z_NO_FLUSH): only deflate stays serial.
 // zlib is the system zlib (1.2.11 in this image, as on the reference's build).
+#include <sched.h>
 #include <zlib.h>
+#include <algorithm>
+#include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <memory>
 #include <vector>
 #include "../../include/rtamd.h"
 
@@ -47,34 +57,50 @@ inline uint8_t paeth(int a, int b, int c) {
 	return static_cast<uint8_t>((pa <= pb && pa <= pc) ? a : (pb <= pc) ? b : c);
 }
 
-// png_write_find_filter: the filtered row (filter byte first) with the smallest cost
-void filter_row(const uint8_t* row, const uint8_t* prev, size_t n, std::vector<uint8_t> cand[5], int& best) {
-	const int bpp = 3;
-	for (int f = 0; f < 5; f++) {
-		cand[f].resize(n + 1);
-		cand[f][0] = static_cast<uint8_t>(f);
-	}
+// png_write_find_filter (pngwutil.c:2323-2700): the filtered row (filter byte first) of the
+// smallest sum of |signed bytes|, the first strict minimum winning.  One pass sums the five
+// candidates' costs, a second writes the chosen one into out[0..n].
+void filter_row(const uint8_t* row, const uint8_t* prev, size_t n, uint8_t* out) {
+	constexpr size_t bpp = 3;
+	uint32_t sum[5] = {0, 0, 0, 0, 0};
 	for (size_t i = 0; i < n; i++) {
-		const int a = i >= static_cast<size_t>(bpp) ? row[i - bpp] : 0;
+		const int a = i >= bpp ? row[i - bpp] : 0;
 		const int b = prev[i];
-		const int c = i >= static_cast<size_t>(bpp) ? prev[i - bpp] : 0;
+		const int c = i >= bpp ? prev[i - bpp] : 0;
 		const int x = row[i];
-		cand[0][i + 1] = static_cast<uint8_t>(x);
-		cand[1][i + 1] = static_cast<uint8_t>(x - a);
-		cand[2][i + 1] = static_cast<uint8_t>(x - b);
-		cand[3][i + 1] = static_cast<uint8_t>(x - ((a + b) >> 1));
-		cand[4][i + 1] = static_cast<uint8_t>(x - paeth(a, b, c));
+		sum[0] += cost(static_cast<uint8_t>(x));
+		sum[1] += cost(static_cast<uint8_t>(x - a));
+		sum[2] += cost(static_cast<uint8_t>(x - b));
+		sum[3] += cost(static_cast<uint8_t>(x - ((a + b) >> 1)));
+		sum[4] += cost(static_cast<uint8_t>(x - paeth(a, b, c)));
 	}
 	uint32_t mins = 0xffffffffu >> 1;  // PNG_MAXSUM
-	best = 0;
-	for (int f = 0; f < 5; f++) {
-		uint32_t sum = 0;
-		for (size_t i = 1; i <= n; i++) sum += cost(cand[f][i]);
-		if (sum < mins) {
-			mins = sum;
+	int best = 0;
+	for (int f = 0; f < 5; f++)
+		if (sum[f] < mins) {
+			mins = sum[f];
 			best = f;
 		}
+	out[0] = static_cast<uint8_t>(best);
+	for (size_t i = 0; i < n; i++) {
+		const int a = i >= bpp ? row[i - bpp] : 0;
+		const int b = prev[i];
+		const int c = i >= bpp ? prev[i - bpp] : 0;
+		const int x = row[i];
+		const int p = best == 0 ? 0 : best == 1 ? a : best == 2 ? b : best == 3 ? ((a + b) >> 1) : paeth(a, b, c);
+		out[i + 1] = static_cast<uint8_t>(x - p);
 	}
+}
+
+// host threads for the row filters: the process's CPUs (the GPU box's share is 16), at most
+// RTAMD_PNG_THREADS when set
+int filter_threads() {
+	int n = 1;
+	cpu_set_t set;
+	if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
+	n = std::min(n, 16);
+	if (const char* e = std::getenv("RTAMD_PNG_THREADS")) n = std::atoi(e);
+	return std::max(1, n);
 }
 
 // optimize_cmf (pngwutil.c:251-288)
@@ -139,15 +165,35 @@ int rt_encode_png(const uint8_t* rgb, int width, int height, std::vector<uint8_t
 		zs.next_out = zbuf.data();
 		zs.avail_out = static_cast<uInt>(zbuf.size());
 	};
-	std::vector<uint8_t> prev(rowbytes, 0), cand[5];
-	for (uint32_t y = 0; y <= h; y++) {
+	// filtered rows, (rowbytes + 1) each: bands of kBand rows taken in order by the threads;
+	// ready[k] is set when band k is written, and the calling thread deflates band after band
+	constexpr uint32_t kBand = 8;
+	const uint32_t n_bands = (h + kBand - 1) / kBand;
+	std::vector<uint8_t> filt((rowbytes + 1) * h);
+	std::unique_ptr<std::atomic<uint8_t>[]> ready(new std::atomic<uint8_t>[n_bands]);
+	for (uint32_t k = 0; k < n_bands; k++) ready[k].store(0, std::memory_order_relaxed);
+	std::atomic<uint32_t> next_band{0};
+	const std::vector<uint8_t> zero_row(rowbytes, 0);
+	auto work = [&]() {
+		for (uint32_t k; (k = next_band.fetch_add(1, std::memory_order_relaxed)) < n_bands;) {
+			for (uint32_t y = k * kBand; y < std::min(h, (k + 1) * kBand); y++)
+				filter_row(rgb + static_cast<size_t>(y) * rowbytes, y ? rgb + static_cast<size_t>(y - 1) * rowbytes : zero_row.data(),
+				           rowbytes, filt.data() + static_cast<size_t>(y) * (rowbytes + 1));
+			ready[k].store(1, std::memory_order_release);
+		}
+	};
+	// small images: no threads (their start costs more than the filtering)
+	const int n_threads = static_cast<size_t>(h) * rowbytes >= (1u << 18) ? std::min<int>(filter_threads(), n_bands) : 0;
+	std::vector<std::thread> pool;
+	for (int t = 0; t < n_threads; t++) pool.emplace_back(work);
+	if (n_threads == 0) work();
+	int rc = RT_OK;
+	for (uint32_t y = 0; y <= h && rc == RT_OK; y++) {
 		const bool finish = y == h;
-		int best = 0;
 		if (!finish) {
-			const uint8_t* row = rgb + static_cast<size_t>(y) * rowbytes;
-			filter_row(row, prev.data(), rowbytes, cand, best);
-			std::memcpy(prev.data(), row, rowbytes);
-			zs.next_in = cand[best].data();
+			if (y % kBand == 0)
+				while (!ready[y / kBand].load(std::memory_order_acquire)) std::this_thread::yield();
+			zs.next_in = filt.data() + static_cast<size_t>(y) * (rowbytes + 1);
 			zs.avail_in = static_cast<uInt>(rowbytes + 1);
 		} else {
 			zs.next_in = nullptr;
@@ -167,10 +213,16 @@ int rt_encode_png(const uint8_t* rgb, int width, int height, std::vector<uint8_t
 			}
 			if (ret == Z_BUF_ERROR && !finish && zs.avail_in == 0) break;
 			if (ret != Z_OK) {
-				deflateEnd(&zs);
-				return RT_ERR_IO;
+				rc = RT_ERR_IO;
+				break;
 			}
 		}
+	}
+	if (rc != RT_OK) next_band.store(n_bands);  // the threads stop at their current band
+	for (std::thread& t : pool) t.join();
+	if (rc != RT_OK) {
+		deflateEnd(&zs);
+		return rc;
 	}
 	deflateEnd(&zs);
 	chunk(out, "IEND", nullptr, 0);

@@ -23,6 +23,7 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DCamera* cam;
 	int32_t n_geoms, n_lights, n_nonambient;
 	int32_t n_may_raise;                      // geometries with DGeom::may_raise
+	int32_t n_meshes;                         // 0: spheres only (the kernels without the mesh search)
 	const int32_t* shadow_light;              // j-th non-ambient light -> light index
 	int32_t work_stats;                       // count the LBVH work (rt_counters node_visits ...); 0 = skip
 };
@@ -156,10 +157,28 @@ hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const Sha
 // device (a fixed grid strides over it)
 hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,
                                hipStream_t stream);
+// Where a fused level (launch_fused) puts its colours: final != 0 (a plan of one traced
+// level): straight into the chunk's output rows (no k_output); else into the level's colours
+// for k_reduce / k_output.  summary != null: the launch's last block reduces the statistics
+// shards into it (launch_stats_finish's work without a launch; `done` counts the finished
+// blocks and is reset by the last one).
+struct FusedOut {
+	int32_t final;
+	int32_t pad;
+	unsigned long long* summary;
+	uint32_t* done;
+};
 // lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output;
-// pixels go to their rows' outputs (fg.rows)
+// pixels go to their rows' outputs (fg.rows); finish non-null: the statistics finish too
 hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
-                         unsigned long long* stats, hipStream_t stream);
+                         unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr = nullptr,
+                         const FusedOut* finish = nullptr);
+// One level in one launch (k_fused): closest hits, children, and every hit's shadow rays and
+// Phong terms from registers (the level's k_closest + k_shadow + k_shade); never for
+// --intersection-only or counting renders.  Arguments as launch_closest.
+hipError_t launch_fused(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
+                        int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr, unsigned long long* stats,
+                        hipStream_t stream, int packet_mask, int plan_last, const FusedOut& fo);
 // End of a render: summary[k] = sum over the shards of statistic k (max for ST_MAX_BITS),
 // summary[ST_COUNT] = the device error word; the shards and the error word are cleared for
 // the next render.

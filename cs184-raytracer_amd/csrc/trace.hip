@@ -48,6 +48,12 @@ constexpr int kShadeBlock = 512;
 #ifndef RT_PACKET_WAVES
 #define RT_PACKET_WAVES RT_TRAVERSAL_WAVES
 #endif
+// A scene of spheres only: no LBVH search, so the closest-hit and per-lane shadow kernels fit
+// 96 VGPRs without spills (5 waves per SIMD; the packet shadow kernel with its fused Phong
+// terms keeps 4: at 96 VGPRs it spills 16)
+#ifndef RT_SPHERE_WAVES
+#define RT_SPHERE_WAVES 5
+#endif
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
 __device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, int W, int H, V3& o, V3& d,
@@ -195,16 +201,51 @@ __device__ __forceinline__ Slots block_append2(bool a, bool b0, bool b1, int32_t
 	             lds.n[1][kMaxWaves] + lds.n[1][wave] + (int)(__popcll(m0 & below) + __popcll(m1 & below))};
 }
 
+// writers.cpp:4-9: (uint8)(min(max(v,0),1) * 255), NaN -> 0
+__device__ __forceinline__ uint8_t to_u8(double v) {
+	v = (1.0 < v) ? 1.0 : v;
+	v = (v < 0.0) ? 0.0 : v;
+	v = v * 255.0;
+	return (v == v) ? (uint8_t)(int)v : (uint8_t)0;
+}
+
+// pixel i of the chunk (column c of its row q) into that row's outputs: f64 and RGB8
+__device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, const double v[3], bool rgb8) {
+	const int64_t q = div_small(i, fg.width);
+	const int64_t c = i - q * fg.width;
+	double* out = fg.rows[q].out;
+	uint8_t* out8 = fg.rows[q].out8;
+	if (out) {
+		out[c * 3 + 0] = v[0];
+		out[c * 3 + 1] = v[1];
+		out[c * 3 + 2] = v[2];
+	}
+	if (out8 && rgb8) {
+		out8[c * 3 + 0] = to_u8(v[0]);
+		out8[c * 3 + 1] = to_u8(v[1]);
+		out8[c * 3 + 2] = to_u8(v[2]);
+	}
+}
+
+template <bool kPacket, bool kMesh, typename DV, typename WS>
+__device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, V3 N, DV dir_of,
+                                               bool inside, int32_t* stack, DeviceCounters* ctr,
+                                               unsigned long long* stats, WS& ws, double col[3]);
+
 // Closest hit (castRay, scene.cpp:142-167) + the bounce decisions of scene.cpp:110-136:
 // the children's rays and the reflective weight depend only on the hit, not on the
 // shading, so they are spawned here and level L+1 can be traced while level L is shaded.
 // One item (thread t of the level's index space) of k_closest; every thread of the block
 // calls it (block_append2 synchronises the block).
-template <bool kPacket, bool kCount>
+// kFused (k_fused): the hit is shaded right here, its shadow rays and Phong terms from the
+// hit held in registers (no hit record, no k_shadow / k_shade launch), and the colour goes
+// where fo says.  Never for --intersection-only.
+template <bool kPacket, bool kCount, bool kMesh, bool kFused = false>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
                                              int remaining, int plan_last, const RayLevel* levels,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
-                                             AppendLds& append_lds, int32_t* stack, uint32_t* stat_lds) {
+                                             AppendLds& append_lds, int32_t* stack, uint32_t* stat_lds,
+                                             const FusedOut* fo = nullptr) {
 	// the level records (~30 buffer pointers) are read where they are used, before and after
 	// the traversal, not held in scalar registers through it
 	const int next_level = remaining > 0 ? level + 1 : level;
@@ -226,9 +267,9 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	if (!kPacket) diag_lanes(0, active);  // [0] wave slots, [1] active lanes of k_closest<false>
 #endif
 	if (kPacket)
-		hit = closest_hit_packet(S, o, d, inside, active, dist, gi, P, Nobj, stack, ctr, ws);
+		hit = closest_hit_packet<kMesh>(S, o, d, inside, active, dist, gi, P, Nobj, stack, ctr, ws);
 	else if (active)
-		hit = closest_hit(S, o, d, inside, dist, gi, P, Nobj, stack, ctr, ws);
+		hit = closest_hit<kMesh>(S, o, d, inside, dist, gi, P, Nobj, stack, ctr, ws);
 	if (active) PROF_END(ws, PH_TOTAL, t_total);
 	flush_stats(ws, stats, 0, kPacket);
 	if (hit) {
@@ -271,7 +312,8 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	const RayLevel* lv = opaque(levels);
 	const auto& cur = *uniform_ptr(lv + level);
 	const auto& next = *uniform_ptr(lv + next_level);
-	const Slots slot = block_append2(shade, spawn_refr, spawn_refl, cur.counts, cur.counts + 1, append_lds);
+	// (a fused level keeps no hit list: its hit counter is not advanced)
+	const Slots slot = block_append2(shade && !kFused, spawn_refr, spawn_refl, cur.counts, cur.counts + 1, append_lds);
 	{
 		const unsigned long long m_hit = __ballot(shade), m_refl = __ballot(spawn_refl), m_refr = __ballot(spawn_refr);
 		if (__lane_id() == 0) {
@@ -281,13 +323,15 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 			if (m_refr) atomicAdd(sh + ST_REFR, (unsigned long long)__popcll(m_refr));
 		}
 	}
-	if (!active) return;
-	cur.hgeom[i] = hit ? gi : -1;
-	if (fg.intersection_only) {  // scene.cpp:69-70
-		const double v = hit ? 1.0 / (dist * dist) : 0.0;
-		cur.cr[i] = cur.cg[i] = cur.cb[i] = v;
-		cur.child_refr[i] = cur.child_refl[i] = -1;
-		return;
+	if (!kFused && !active) return;
+	if (!kFused) {
+		cur.hgeom[i] = hit ? gi : -1;
+		if (fg.intersection_only) {  // scene.cpp:69-70
+			const double v = hit ? 1.0 / (dist * dist) : 0.0;
+			cur.cr[i] = cur.cg[i] = cur.cb[i] = v;
+			cur.child_refr[i] = cur.child_refl[i] = -1;
+			return;
+		}
 	}
 	int32_t refr_idx = -1, refl_idx = -1;
 	// the next level holds at most next.capacity rays: a child beyond it is not written and
@@ -321,8 +365,28 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 		cur.kg[i] = kr[1];
 		cur.kb[i] = kr[2];
 	}
-	cur.child_refr[i] = refr_idx;
-	cur.child_refl[i] = refl_idx;
+	if (!kFused || !fo->final) {
+		if (active) {
+			cur.child_refr[i] = refr_idx;
+			cur.child_refl[i] = refl_idx;
+		}
+	}
+	if constexpr (kFused) {
+		// every lane of the wave takes part (the packet shadow searches are wave-uniform); a
+		// miss is black (scene.cpp:66-67)
+		WorkStats<false> ws{};
+		double col[3] = {0.0, 0.0, 0.0};
+		shade_in_place<kPacket, kMesh>(S, shade, gi, P, N, [&]() { return d; }, inside, stack, ctr, stats, ws, col);
+		if (!active) return;
+		if (fo->final) {
+			write_pixel(fg, i, col, true);
+		} else {
+			cur.cr[i] = col[0];
+			cur.cg[i] = col[1];
+			cur.cb[i] = col[2];
+		}
+		return;
+	}
 	if (!hit) {  // background: black (scene.cpp:66-67); hits are coloured by k_shade
 		cur.cr[i] = cur.cg[i] = cur.cb[i] = 0.0;
 		return;
@@ -346,17 +410,18 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 // before the host knows their size: the ray count is read from the previous level's
 // child counter (n_dev) and a fixed grid strides over it, so each level is queued behind
 // the previous one without a host round trip.
-template <bool kPacket, bool kCount>
+template <bool kPacket, bool kCount, bool kMesh>
 __global__ void __launch_bounds__(kBlock)
-    __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
+    __attribute__((amdgpu_waves_per_eu(!kMesh ? RT_SPHERE_WAVES : kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
                                                                       int64_t n_host, const int32_t* n_dev,
                                                                       int remaining, int plan_last,
                                                                       const RayLevel* levels, DeviceCounters* ctr,
                                                                       unsigned long long* stats) {
 	__shared__ AppendLds append_lds;
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
-	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
-	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	// the traversal stacks (LBVH searches: none in a scene of spheres only)
+	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
 	// level records read through the constant address space (scalar loads at their uses)
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -371,9 +436,98 @@ __global__ void __launch_bounds__(kBlock)
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
-		closest_item<kPacket, kCount>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
+		closest_item<kPacket, kCount, kMesh>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
 		                      append_lds, stack, stat_lds);
 	}
+}
+
+__device__ __forceinline__ bool stat_is_max(int k) { return k == ST_MAX_BITS || k == ST_MAXNODES0 || k == ST_MAXNODES1; }
+
+// The statistics reduction by the last block of a launch (FusedOut::summary): k_stats_finish's
+// work without a launch of its own.  Every block has added into the shards with device-scope
+// atomics (performed beyond the XCDs' L2s, MI355X_MICROARCH.md "Inter-workgroup
+// visibility"); each wave waits for its own to complete, the block then counts itself done on
+// one device-scope counter, and the block whose add returns the last count reduces the shards
+// (sc1 loads, L2-bypassing) into the summary (pinned host memory), clears them and the error
+// word for the next render and resets the counter.  No L2 write-back or invalidation: the
+// only data handed over are those atomics.  Every thread of the block calls it (api.cpp keeps
+// it to grids of at most 2048 blocks: one counter takes ~88 adds per us).
+__device__ void last_block_finish(unsigned long long* stats, DeviceCounters* ctr, const FusedOut& fo) {
+	__shared__ uint32_t last;
+	__shared__ unsigned long long part[kMaxWaves][ST_COUNT];
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics are performed
+	__syncthreads();
+	if (threadIdx.x == 0)
+		last = __hip_atomic_fetch_add(fo.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+	__syncthreads();
+	if (!last) return;
+	unsigned long long v[ST_COUNT];
+#pragma unroll
+	for (int k = 0; k < ST_COUNT; k++) v[k] = 0;
+	for (int sh = threadIdx.x; sh < kStatShards; sh += blockDim.x) {
+		unsigned long long* p = stats + sh * kStatStride;
+#pragma unroll
+		for (int k = 0; k < ST_COUNT; k++) {
+			const unsigned long long x = __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+			v[k] = stat_is_max(k) ? (x > v[k] ? x : v[k]) : v[k] + x;
+		}
+#pragma unroll
+		for (int k = 0; k < ST_COUNT; k++) p[k] = 0;
+	}
+	const int w = threadIdx.x >> 6;
+#pragma unroll
+	for (int k = 0; k < ST_COUNT; k++) {
+		for (int off = 32; off > 0; off >>= 1) {
+			const unsigned long long o = __shfl_xor(v[k], off);
+			v[k] = stat_is_max(k) ? (o > v[k] ? o : v[k]) : v[k] + o;
+		}
+		if (__lane_id() == 0) part[w][k] = v[k];
+	}
+	__syncthreads();
+	const int t = threadIdx.x, nw = (blockDim.x + 63) >> 6;
+	if (t < ST_COUNT) {
+		unsigned long long r = part[0][t];
+		for (int q = 1; q < nw; q++) r = stat_is_max(t) ? (part[q][t] > r ? part[q][t] : r) : r + part[q][t];
+		fo.summary[t] = r;
+	}
+	if (t == ST_COUNT) {
+		fo.summary[t] = static_cast<unsigned long long>(
+		    __hip_atomic_load(&ctr->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+		ctr->error = 0;
+		*fo.done = 0;
+	}
+	// the summary is pinned host memory: visible at system scope before the kernel completes
+	__threadfence_system();
+}
+
+// A whole level in one launch (small chunks and plans of one traced level, api.cpp): closest
+// hits, children, and each hit's shadow rays and Phong terms from registers
+// (closest_item<.., kFused>), with fo.final the output pixels too, and with fo.summary the
+// statistics finish.  Level 0 traces 8x8 tiles as wave packets like k_closest.
+#ifndef RT_FUSED_WAVES
+#define RT_FUSED_WAVES 4
+#endif
+template <bool kPacket, bool kMesh>
+__global__ void __launch_bounds__(kBlock)
+    __attribute__((amdgpu_waves_per_eu(RT_FUSED_WAVES))) k_fused(
+        DeviceScene S, FrameGeometry fg, int level, int64_t n_host, const int32_t* n_dev, int remaining, int plan_last,
+        const RayLevel* levels, DeviceCounters* ctr, unsigned long long* stats, FusedOut fo) {
+	__shared__ AppendLds append_lds;
+	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	const auto& cur0 = *uniform_ptr(levels + level);
+	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
+	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur0.capacity) : n_host;
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		if (remaining > 0) next0.counts[0] = next0.counts[1] = 0;
+		if (n) atomicAdd(stats + ST_RAYS, static_cast<unsigned long long>(n));
+	}
+	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride)
+		closest_item<kPacket, false, kMesh, true>(S, fg, level, n, remaining, plan_last, levels, ctr, stats,
+		                                          base + threadIdx.x, append_lds, stack, nullptr, &fo);
+	if (fo.summary) last_block_finish(stats, ctr, fo);
 }
 
 // Level of item t of a batch (wave-uniform: every level's items start on a wave boundary,
@@ -422,15 +576,14 @@ __device__ __forceinline__ int64_t batch_total(const ShadeBatch& B, int nl) {
 	return tot;
 }
 
-// Phong terms in light order (scene.cpp:78-108) of hit slot hs (hit point P, shading normal
-// N, viewing direction d); occluded_j(j): the verdict of the j-th non-ambient light.
-template <typename LV, typename OCC>
-__device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, int64_t hs, V3 P, V3 N, V3 d,
-                                          OCC occluded_j, const double* log_tab, const uint64_t* exp_tab,
-                                          DeviceCounters* ctr) {
-	const int64_t i = cur.hit_list[hs];
-	const int gi = cur.hgeom[i];
-	double col[3] = {0.0, 0.0, 0.0};
+// Phong terms in light order (scene.cpp:78-108) of a hit on geometry gi (hit point P,
+// shading normal N, viewing direction d); occluded_j(j): the verdict of the j-th non-ambient
+// light.  The colour goes to col.
+template <typename OCC>
+__device__ __forceinline__ void phong(const DeviceScene& S, int gi, V3 P, V3 N, V3 d, OCC occluded_j,
+                                      const double* log_tab, const uint64_t* exp_tab, DeviceCounters* ctr,
+                                      double col[3]) {
+	col[0] = col[1] = col[2] = 0.0;
 	const DMaterial& M = S.mats[S.geoms[gi].mat];
 	int j = 0;
 	for (int li = 0; li < S.n_lights; li++) {
@@ -463,9 +616,82 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 #pragma unroll
 		for (int k = 0; k < 3; k++) col[k] = col[k] + (spec * att[k]) * M.ks[k];
 	}
+}
+// the same for hit slot hs of a level (hit records, compacted), into the ray's colour
+template <typename LV, typename OCC>
+__device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, int64_t hs, V3 P, V3 N, V3 d,
+                                          OCC occluded_j, const double* log_tab, const uint64_t* exp_tab,
+                                          DeviceCounters* ctr) {
+	const int64_t i = cur.hit_list[hs];
+	double col[3];
+	phong(S, cur.hgeom[i], P, N, d, occluded_j, log_tab, exp_tab, ctr, col);
 	cur.cr[i] = col[0];
 	cur.cg[i] = col[1];
 	cur.cb[i] = col[2];
+}
+
+// The shadow verdict of the j-th non-ambient light for a hit at P with shading normal N
+// (scene.cpp:87-93): occluded, or both Phong terms exact zeros.  Both Phong terms of this
+// light (scene.cpp:96-106, the expressions of k_shade) are exact zeros when max(N.L, 0) and
+// max(-V.R, 0) are (given ns > 0 and finite colours, DMaterial/DLight::zero_terms): the
+// colour is the same bits whether the light is occluded or not (it is never -0), so that ray
+// is not traced.  dv_of(): the viewing direction, read only for that test.  Every lane of
+// the wave calls it (kPacket: the search is wave-uniform; lanes without a hit pass on false).
+template <bool kPacket, bool kMesh, typename DV, typename WS>
+__device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P, V3 N, bool inside, bool zero_mat,
+                                              bool on, DV dv_of, int32_t* stack, DeviceCounters* ctr,
+                                              unsigned long long* stats, WS& ws) {
+	V3 Ld = mk(0, 0, 1);
+	bool rev = false, zero = false;
+	double dL = 0;
+	if (on) {
+		const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
+		const bool point = L.kind == DLIGHT_POINT;
+		const V3 lv = load3(L.vec);
+		Ld = ray_dir(point ? lv - P : -lv, ctr);  // Light::calculateRayToLight
+		const double nl_dot = dot4z(N, Ld);
+		rev = (nl_dot < 0) ^ inside;
+		dL = point ? sqrt(sq4(lv - P)) : INFINITY;
+		if (zero_mat && L.zero_terms && nl_dot <= 0.0) {
+			const V3 R = (2 * nl_dot) * N - Ld;
+			zero = -dot4z(dv_of(), R) <= 0.0;
+		}
+		// the reference's castRay still maps the ray into every object space (may raise)
+		if (zero) check_may_raise(S, Ld, true, ctr);
+	}
+	const bool trace = on && !zero;
+#if RT_DIAG_LANES
+	if (!kPacket) {
+		diag_lanes(16, on);     // [16] wave slots, [17] lanes with a hit of this level
+		diag_lanes(18, trace);  // [18] wave slots, [19] lanes tracing (zero-term decided excluded)
+	}
+#endif
+	bool occ = false;
+	if (kPacket)
+		occ = occluded_packet<kMesh>(S, P, Ld, rev, dL, trace, stack, ctr, ws);
+	else if (trace)
+		occ = occluded<kMesh>(S, P, Ld, rev, dL, stack, ctr, ws);
+	const unsigned long long mz = __ballot(zero);
+	if (mz && __lane_id() == 0) atomicAdd(shard(stats) + ST_SHADOW_ZERO, (unsigned long long)__popcll(mz));
+	return occ || zero;
+}
+
+// A fused level's shading (closest_item<.., kFused>): the verdicts of every light for the
+// hit held in registers, then its Phong terms (scene.cpp:78-108) into col.  on: the lane has
+// a hit to shade (every lane of the wave calls it).
+template <bool kPacket, bool kMesh, typename DV, typename WS>
+__device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, V3 N, DV dir_of,
+                                               bool inside, int32_t* stack, DeviceCounters* ctr,
+                                               unsigned long long* stats, WS& ws, double col[3]) {
+	const bool zero_mat = on && S.mats[S.geoms[gi].mat].zero_terms;
+	unsigned long long verdicts = 0;  // bit j: the j-th non-ambient light's verdict (<= 64 lights)
+	for (int j = 0; j < S.n_nonambient; j++)
+		verdicts |= static_cast<unsigned long long>(
+		                light_verdict<kPacket, kMesh>(S, j, P, N, inside, zero_mat, on, dir_of, stack, ctr, stats, ws))
+		            << j;
+	if (on)
+		phong(S, gi, P, N, dir_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
+		      glibc_pow_data::kLogTab, glibc_pow_data::kExpTab, ctr, col);
 }
 
 // Shadow rays (scene.cpp:87-93), two item layouts (ShadeBatch::all_lights):
@@ -475,7 +701,7 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 //    towards each light in turn (one light at a time, still wave-uniform), loading the hit
 //    records once for all lights.
 // The light record of the wave is read with scalar loads.
-template <bool kPacket, bool kCount>
+template <bool kPacket, bool kCount, bool kMesh>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
                                             uint32_t* stat_lds) {
@@ -515,52 +741,17 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	}
 	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
 	for (int j = j0; j < j1; j++) {
-		V3 Ld = mk(0, 0, 1);
-		bool rev = false, zero = false;
-		double dL = 0;
-		if (on) {
-			const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
-			const bool point = L.kind == DLIGHT_POINT;
-			const V3 lv = load3(L.vec);
-			Ld = ray_dir(point ? lv - P : -lv, ctr);  // Light::calculateRayToLight
-			const double nl_dot = dot4z(N, Ld);
-			rev = (nl_dot < 0) ^ inside;
-			dL = point ? sqrt(sq4(lv - P)) : INFINITY;
-			// Both Phong terms of this light (scene.cpp:96-106, the expressions of k_shade)
-			// are exact zeros when max(N.L, 0) and max(-V.R, 0) are (given ns > 0 and finite
-			// colours, DMaterial/DLight::zero_terms): the colour is the same bits whether
-			// the light is occluded or not (it is never -0), so the ray is not traced.
-			if (zero_mat && L.zero_terms && nl_dot <= 0.0) {
-				const V3 R = (2 * nl_dot) * N - Ld;
-				const auto& cur = *uniform_ptr(opaque(levels) + level);
-				const V3 dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
-				zero = -dot4z(dv, R) <= 0.0;
-			}
-			// the reference's castRay still maps the ray into every object space (may raise)
-			if (zero) check_may_raise(S, Ld, true, ctr);
-			PROF_END(ws, PH_SETUP, t_total);
-		}
-		const bool trace = on && !zero;
-#if RT_DIAG_LANES
-		if (!kPacket) {
-			diag_lanes(16, on);     // [16] wave slots, [17] lanes with a hit of this level
-			diag_lanes(18, trace);  // [18] wave slots, [19] lanes tracing (zero-term decided excluded)
-		}
-#endif
-		bool occ = false;
-		if (kPacket)
-			occ = occluded_packet(S, P, Ld, rev, dL, trace, stack, ctr, ws);
-		else if (trace)
-			occ = occluded(S, P, Ld, rev, dL, stack, ctr, ws);
+		const bool v = light_verdict<kPacket, kMesh>(S, j, P, N, inside, zero_mat, on, [&]() {
+			const auto& cur = *uniform_ptr(opaque(levels) + level);
+			return mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
+		}, stack, ctr, stats, ws);
 		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
 		if (B.fused) {
-			verdicts |= static_cast<unsigned long long>(occ || zero) << j;
+			verdicts |= static_cast<unsigned long long>(v) << j;
 		} else if (on) {
 			const auto& cur = *uniform_ptr(opaque(levels) + level);
-			cur.occl[j * cur.capacity + h] = occ || zero;
+			cur.occl[j * cur.capacity + h] = v;
 		}
-		const unsigned long long mz = __ballot(zero);
-		if (mz && __lane_id() == 0) atomicAdd(shard(stats) + ST_SHADOW_ZERO, (unsigned long long)__popcll(mz));
 	}
 	if (on) PROF_END(ws, PH_TOTAL, t_total);
 	flush_stats(ws, stats, 1, kPacket);
@@ -576,18 +767,18 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 
 // Host-counted batches launch one thread per item; device-counted ones a fixed grid that
 // strides over the items (the bound is block-uniform: no lane of a wave leaves early).
-template <bool kPacket, bool kCount>
+template <bool kPacket, bool kCount, bool kMesh>
 __global__ void __launch_bounds__(kBlock)
-    __attribute__((amdgpu_waves_per_eu(kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
+    __attribute__((amdgpu_waves_per_eu(!kMesh && !kPacket ? RT_SPHERE_WAVES : kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
-	__shared__ int32_t stack_mem[kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
-	int32_t* stack = kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
-		shadow_item<kPacket, kCount>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
+		shadow_item<kPacket, kCount, kMesh>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -646,29 +837,12 @@ __global__ void k_reduce(int64_t n_host, const int32_t* n_dev, RayLevel cur, Ray
 	}
 }
 
-// writers.cpp:4-9: (uint8)(min(max(v,0),1) * 255), NaN -> 0
-__device__ __forceinline__ uint8_t to_u8(double v) {
-	v = (1.0 < v) ? 1.0 : v;
-	v = (v < 0.0) ? 0.0 : v;
-	v = v * 255.0;
-	return (v == v) ? (uint8_t)(int)v : (uint8_t)0;
-}
-
 // the image: level 0's colours, reduced with level 1 on the fly when `reduce` (the last
-// k_reduce fused into the output)
+// k_reduce fused into the output); fo.summary: the last block finishes the statistics
 __global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lvl1, int32_t reduce,
-                         unsigned long long* stats) {
+                         unsigned long long* stats, DeviceCounters* ctr, FusedOut fo) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const int32_t io = fg.intersection_only;
-	double* out = nullptr;
-	uint8_t* out8 = nullptr;
-	int64_t c = 0;
-	if (i < n) {  // pixel i: column c of the chunk's row q, written to that row's outputs
-		const int64_t q = div_small(i, fg.width);
-		c = i - q * fg.width;
-		out = fg.rows[q].out;
-		out8 = fg.rows[q].out8;
-	}
 	// level 0's counts were read back; clear them for the lane's next chunk
 	if (i == 0) lvl0.counts[0] = lvl0.counts[1] = 0;
 	double v[3] = {0, 0, 0};
@@ -680,16 +854,7 @@ __global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lv
 			v[1] = lvl0.cg[i];
 			v[2] = lvl0.cb[i];
 		}
-		if (out) {
-			out[c * 3 + 0] = v[0];
-			out[c * 3 + 1] = v[1];
-			out[c * 3 + 2] = v[2];
-		}
-		if (out8 && !io) {
-			out8[c * 3 + 0] = to_u8(v[0]);
-			out8[c * 3 + 1] = to_u8(v[1]);
-			out8[c * 3 + 2] = to_u8(v[2]);
-		}
+		write_pixel(fg, i, v, !io);
 	}
 	if (io) {  // running max of maxCoeff over positive doubles (bit order == value order)
 		const double m = (i < n) ? fmax(fmax(v[0], v[1]), v[2]) : 0.0;
@@ -700,6 +865,7 @@ __global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lv
 		}
 		if (__lane_id() == 0 && bits) atomicMax(shard(stats) + ST_MAX_BITS, bits);
 	}
+	if (fo.summary) last_block_finish(stats, ctr, fo);
 }
 
 // one block of kStatShards threads: thread t owns shard t; tree reduction in LDS
@@ -917,10 +1083,17 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
 		                   plan_last, levels_dev, ctr, stats);
 	};
-	if (packet)
-		s.work_stats ? go(k_closest<true, true>) : go(k_closest<true, false>);
-	else
-		s.work_stats ? go(k_closest<false, true>) : go(k_closest<false, false>);
+	// instantiations: packet or per lane, counting or not, with or without the mesh search
+	if (s.n_meshes == 0) {
+		if (packet)
+			s.work_stats ? go(k_closest<true, true, false>) : go(k_closest<true, false, false>);
+		else
+			s.work_stats ? go(k_closest<false, true, false>) : go(k_closest<false, false, false>);
+	} else if (packet) {
+		s.work_stats ? go(k_closest<true, true, true>) : go(k_closest<true, false, true>);
+	} else {
+		s.work_stats ? go(k_closest<false, true, true>) : go(k_closest<false, false, true>);
+	}
 	return hipGetLastError();
 }
 
@@ -948,10 +1121,16 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 	auto go = [&](auto kernel) {
 		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
 	};
-	if (shadow_packet(b, packet_mask))
-		s.work_stats ? go(k_shadow<true, true>) : go(k_shadow<true, false>);
-	else
-		s.work_stats ? go(k_shadow<false, true>) : go(k_shadow<false, false>);
+	if (s.n_meshes == 0) {
+		if (shadow_packet(b, packet_mask))
+			s.work_stats ? go(k_shadow<true, true, false>) : go(k_shadow<true, false, false>);
+		else
+			s.work_stats ? go(k_shadow<false, true, false>) : go(k_shadow<false, false, false>);
+	} else if (shadow_packet(b, packet_mask)) {
+		s.work_stats ? go(k_shadow<true, true, true>) : go(k_shadow<true, false, true>);
+	} else {
+		s.work_stats ? go(k_shadow<false, true, true>) : go(k_shadow<false, false, true>);
+	}
 	return hipGetLastError();
 }
 
@@ -973,10 +1152,30 @@ hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& 
 }
 
 hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
-                         unsigned long long* stats, hipStream_t stream) {
+                         unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr, const FusedOut* finish) {
 	if (n <= 0) return hipSuccess;
+	const FusedOut fo = finish ? *finish : FusedOut{};
 	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, fg, lvl0, lvl1 ? *lvl1 : lvl0,
-	                   lvl1 ? 1 : 0, stats);
+	                   lvl1 ? 1 : 0, stats, ctr, fo);
+	return hipGetLastError();
+}
+
+hipError_t launch_fused(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
+                        int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr, unsigned long long* stats,
+                        hipStream_t stream, int packet_mask, int plan_last, const FusedOut& fo) {
+	if (n <= 0) return hipSuccess;
+	const bool packet = packet_mask & (level == 0 ? kPacketClosest0 : level == 1 ? kPacketClosestN | kPacketClosest1 : kPacketClosestN);
+	const int64_t threads = (level == 0 && packet) ? tile_threads(n, fg.width) : n;
+	const unsigned grid = n_dev ? (unsigned)std::min<int64_t>(grid_for(threads, kBlock), kStrideBlocks)
+	                            : grid_for(threads, kBlock);
+	auto go = [&](auto kernel) {
+		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
+		                   plan_last, levels_dev, ctr, stats, fo);
+	};
+	if (s.n_meshes == 0)
+		packet ? go(k_fused<true, false>) : go(k_fused<false, false>);
+	else
+		packet ? go(k_fused<true, true>) : go(k_fused<false, true>);
 	return hipGetLastError();
 }
 

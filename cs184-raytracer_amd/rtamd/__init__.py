@@ -68,13 +68,15 @@ class rt_counters(ctypes.Structure):
                 ("stage_launches", ctypes.c_int32 * 3), ("stage_node_visits", ctypes.c_int64 * 2),
                 ("stage_tri_tests", ctypes.c_int64 * 2), ("stage_candidates", ctypes.c_int64 * 2),
                 ("stage_sphere_tests", ctypes.c_int64 * 2), ("stage_bvh_traversals", ctypes.c_int64 * 2),
-                ("stage_max_node_visits", ctypes.c_int64 * 2), ("shadow_rays_zero_terms", ctypes.c_int64)]
+                ("stage_max_node_visits", ctypes.c_int64 * 2), ("shadow_rays_zero_terms", ctypes.c_int64),
+                ("host_ms", ctypes.c_double), ("copy_ms", ctypes.c_double)]
 
 
 class rt_scene_info(ctypes.Structure):
     _fields_ = [("n_geometries", ctypes.c_int32), ("n_spheres", ctypes.c_int32), ("n_meshes", ctypes.c_int32),
                 ("n_lights", ctypes.c_int32), ("n_faces", ctypes.c_int64), ("n_bvh_nodes", ctypes.c_int64),
-                ("device_bytes", ctypes.c_int64), ("max_bvh_depth", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("device_bytes", ctypes.c_int64), ("max_bvh_depth", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("level_bytes", ctypes.c_int64), ("build_ms", ctypes.c_double), ("upload_ms", ctypes.c_double)]
 
 
 class rt_xform_desc(ctypes.Structure):

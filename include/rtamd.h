@@ -59,6 +59,10 @@ typedef struct rt_scene_info {
 	int64_t device_bytes;    /* HBM held by the uploaded scene                        */
 	int32_t max_bvh_depth;   /* deepest LBVH (root = depth 0)                          */
 	int32_t reserved;
+	int64_t level_bytes;     /* HBM held by the ray-level buffers of the renders so far
+	                            (grown on demand, kept for later renders)              */
+	double  build_ms;        /* host time of rt_scene_create's LBVH build + flattening  */
+	double  upload_ms;       /* host time of its HBM allocations, copies and set-up     */
 } rt_scene_info;
 
 /* ---------------------------------------------------------------- flat scene descriptor */
@@ -200,6 +204,8 @@ typedef struct rt_counters {
 	int64_t shadow_rays_zero_terms;    /* shadow rays (counted in shadow_rays) whose diffuse and
 	                                      specular terms are exact zeros, so the verdict cannot
 	                                      change the colour: decided without traversal         */
+	double  host_ms;   /* wall time of the call on the host, entry to return                 */
+	double  copy_ms;   /* of which the image's device-to-host copy (rt_render, rt_render_rgb8) */
 } rt_counters;
 
 /* Scene::renderScene into a caller-owned host buffer of n_rows*W*3 doubles

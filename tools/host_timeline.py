@@ -26,22 +26,22 @@ def kname(r):
     return m.group(1) if m else r["Kernel_Name"][:24]
 
 
-# frames end with the statistics reduction; the last frame starts after the API call that
-# waited for the previous one (the synchronisation that returned after k_stats_finish)
-fin = [r for r in ker if "k_stats_finish" in r["Kernel_Name"]]
-prev_end, last_end = int(fin[-2]["End_Timestamp"]), int(fin[-1]["End_Timestamp"])
-# the render call's API calls: after the previous frame's synchronisation returned
-calls = [r for r in api if int(r["Start_Timestamp"]) > prev_end and int(r["Start_Timestamp"]) <= last_end + 200000]
-sync_after = [r for r in calls if r["Function"] in ("hipStreamSynchronize", "hipDeviceSynchronize")]
+# frames: tools/one_config.py synchronises before every render (hipDeviceSynchronize) and
+# rt_scene_destroy once more at the end; the last frame lies between the last two
+syncs = [r for r in api if r["Function"] == "hipDeviceSynchronize"]
+prev_end, last_end = int(syncs[-2]["Start_Timestamp"]), int(syncs[-1]["Start_Timestamp"])
+calls = [r for r in api if prev_end <= int(r["Start_Timestamp"]) < last_end]
 t0 = int(calls[0]["Start_Timestamp"])
 ev = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "api", r["Function"]) for r in calls]
-ev += [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "gpu", kname(r)) for r in ker
+ev += [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "gpu",
+        "%-26s q%s s%s" % (kname(r), r.get("Queue_Id", "?"), r.get("Stream_Id", "?"))) for r in ker
        if prev_end < int(r["Start_Timestamp"]) <= last_end]
 ev.sort()
 for s, e, k, n in ev:
     print(f"{k} {n:34s} start={(s - t0) / 1e3:8.1f}us dur={(e - s) / 1e3:7.1f}us")
 first_k = min(s for s, e, k, n in ev if k == "gpu")
 last_api = max(e for s, e, k, n in ev if k == "api")
+last_k = max(e for s, e, k, n in ev if k == "gpu")
 print(f"first API call -> first kernel start {(first_k - t0) / 1e3:.1f} us; last kernel end "
-      f"{(last_end - t0) / 1e3:.1f} us; last API call returns {(last_api - t0) / 1e3:.1f} us")
+      f"{(last_k - t0) / 1e3:.1f} us; last API call returns {(last_api - t0) / 1e3:.1f} us")
 print(f"API calls {len(calls)}; host time in API calls {sum(e - s for s, e, k, n in ev if k == 'api') / 1e3:.1f} us")
