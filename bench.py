@@ -576,8 +576,9 @@ def main():
     from rtamd import dist as rd
     from rtamd.configs import CONFIGS, SCENES, option_kwargs
 
-    if a.backend == "gloo":
-        local = local % torch.cuda.device_count()  # rehearsal: several ranks may share a GPU
+    # more ranks than visible GPUs share them (a gloo rehearsal); over RCCL rank_topology then
+    # stops the run with a message instead of a device-ordinal error
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         with stdout_to_stderr():

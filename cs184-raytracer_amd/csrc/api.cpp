@@ -22,6 +22,7 @@ extern "C" int rt_encode_png(const uint8_t* rgb, int width, int height, std::vec
 namespace {
 
 thread_local std::string g_error;
+constexpr size_t kFinDoneBytes = 9 * 128;  // rt_scene::fin_done: top + 8 per-XCD counters (trace.hip)
 
 int fail(int code, const std::string& msg) {
 	g_error = msg;
@@ -147,6 +148,7 @@ struct Lane {
 	// k_shadow + k_shade of level L < direct_levels on shade[L % 3]; the small deep levels
 	// are shaded in batches on shade[3] once the chain has finished
 	hipStream_t shade[4] = {nullptr, nullptr, nullptr, nullptr};
+	int prio_low = 0;
 	std::vector<LevelBuffers> levels;
 	// RayLevel records of all levels, read by the kernels through the constant address space
 	// (pinned host copy + device copy, updated in stream order when a level is reallocated)
@@ -259,7 +261,7 @@ struct rt_scene {
 	// (no fork/join across queues) and its last kernel finishes the statistics (no
 	// k_stats_finish launch)
 	int direct = 1;
-	uint32_t* fin_done = nullptr;  // device: blocks done of a launch that finishes the statistics
+	uint32_t* fin_done = nullptr;  // device: blocks done of a launch that finishes the statistics (9 x 128 B)
 	int all_lights_for(int first_level, int64_t hits, int64_t light_major_below) const {
 		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
 		if (al && ds.n_nonambient > 1 && hits < light_major_below) al = 0;
@@ -385,14 +387,26 @@ int ensure_events(Lane& ln, size_t level) {
 	return RT_OK;
 }
 
+// shading stream k of a lane, made at its first use: a stream costs 7-11 ms to create
+// (profiles/round4: host traces), and a render of one traced level uses one of the four
+hipStream_t shade_stream(Lane& ln, int k) {
+	if (!ln.shade[k]) {
+		if (hipStreamCreateWithPriority(&ln.shade[k], hipStreamNonBlocking, ln.prio_low) != hipSuccess) {
+			ln.shade[k] = nullptr;
+			return nullptr;
+		}
+		roctxNameHipStream("rtamd lane: shading", ln.shade[k]);
+	}
+	return ln.shade[k];
+}
+
 int lane_create(Lane& ln, int prio_low, int prio_high) {
 	HIP_TRY(hipStreamCreateWithPriority(&ln.stream, hipStreamNonBlocking, prio_high));
 	HIP_TRY(hipStreamCreateWithPriority(&ln.readback, hipStreamNonBlocking, prio_high));
-	for (hipStream_t& q : ln.shade) HIP_TRY(hipStreamCreateWithPriority(&q, hipStreamNonBlocking, prio_low));
+	ln.prio_low = prio_low;  // the shading streams are made at their first use (shade_stream)
 	HIP_TRY(hipEventCreateWithFlags(&ln.chunk_done, hipEventDisableTiming));
 	roctxNameHipStream("rtamd lane: k_closest chain", ln.stream);
 	roctxNameHipStream("rtamd lane: level counts read-back", ln.readback);
-	for (hipStream_t q : ln.shade) roctxNameHipStream("rtamd lane: shading", q);
 	return RT_OK;
 }
 
@@ -436,7 +450,7 @@ struct Render {
 	bool direct_ok = false;    // the call is one chunk on one lane: it may run on the caller's stream
 	bool stats_fused = false;  // the call's last kernel finishes the statistics (no k_stats_finish)
 	bool finished = false;     // the plan issued last attached the statistics finish to a launch
-	static constexpr int64_t kFinishBlocks = 2048;
+	static constexpr int64_t kFinishBlocks = int64_t(1) << 30;
 
 	// the caller's prior work before any of this lane's (the fork), once per call; a chunk
 	// on the caller's own stream needs none
@@ -611,16 +625,14 @@ struct Render {
 		// A plan of one traced level (no bounce: bdepth 0, or nothing reflective was hit) has
 		// nothing to overlap either: C2a 0.185 -> 0.179, C2b 0.334 -> 0.327, C4 0.357 -> 0.355 ms,
 		// C4 2-way share 0.302 -> 0.290 ms (RTAMD_ONE_STREAM_LEVEL1)
-		// the statistics finish inside the last launch (finish: a call of this one chunk), where
-		// that launch has at most kFinishBlocks blocks: every block counts itself done on one
-		// device-scope counter, which takes ~88 atomics per us (MI355X_MICROARCH.md "dequeue");
-		// a larger grid leaves the finish to k_stats_finish on the same stream
+		// the statistics finish inside the last launch (finish: a call of this one chunk): every
+		// block counts itself done (per-XCD counters, trace.hip last_block_finish)
 		rtamd::FusedOut fin{};
 		fin.summary = s->summary_mapped;
 		fin.done = s->fin_done;
 		finished = false;
 		auto finish_on = [&](int64_t threads, int block) {
-			const bool on = finish && (threads + block - 1) / block <= kFinishBlocks;
+			const bool on = finish && (threads + block - 1) / block <= kFinishBlocks;  // (grid sizes: unsigned)
 			finished = finished || on;
 			return on;
 		};
@@ -686,7 +698,8 @@ struct Render {
 				// wait on a not yet signalled event of another queue costs tens of microseconds
 				if (L < direct_levels && rc == RT_OK) {
 					const bool side = L < nlev - 1;
-					hipStream_t q = side ? ln.shade[L % 3] : st;
+					hipStream_t q = side ? shade_stream(ln, L % 3) : st;
+					if (!q) step(hipErrorOutOfMemory);
 					if (side) step(hipStreamWaitEvent(q, done, 0));
 					scratch.launches[1] = scratch.launches[2] = 0;
 					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch);
@@ -853,9 +866,10 @@ struct Render {
 		ln.deferred.clear();
 		ln.planned = nullptr;
 		Plan* pl = find_plan(ln, key_of(ln));
-		// the call's only chunk, replaying a plan of this lane's own on one stream: it runs on
-		// the caller's stream (no fork, no join); otherwise on the lane's streams after the fork
-		ln.direct = s->direct && direct_ok && pl && !pl->exec && one_stream(ln, *pl);
+		// the call's only chunk, replaying a plan of this lane's own: its chain runs on the
+		// caller's stream (no fork, no join; side streams wait on its events as before);
+		// otherwise on the lane's streams after the fork
+		ln.direct = s->direct && direct_ok && pl && !pl->exec;
 		const hipStream_t st = ln.direct ? caller : ln.stream;
 		if (!ln.direct && (rc = fork(ln))) return rc;
 		if (copy_rows)
@@ -903,7 +917,9 @@ struct Render {
 		}
 		if (nh > 0) {
 			if (L < direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
-				if ((rc = launch_shading(ln, {{L, nh}}, ln.shade[L % 3]))) return rc;
+				hipStream_t q = shade_stream(ln, L % 3);
+				if (!q) return fail(RT_ERR_DEVICE, "shading stream creation failed");
+				if ((rc = launch_shading(ln, {{L, nh}}, q))) return rc;
 			} else {
 				ln.deferred.push_back({L, nh});
 			}
@@ -911,7 +927,9 @@ struct Render {
 		if (more) return RT_OK;
 		for (size_t k = 0, e; k < ln.deferred.size(); k = e) {
 			e = std::min(ln.deferred.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
-			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, ln.shade[3]))) return rc;
+			hipStream_t q = shade_stream(ln, 3);
+			if (!q) return fail(RT_ERR_DEVICE, "shading stream creation failed");
+			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, q))) return rc;
 		}
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
 		// colours reduced bottom-up; level 0's reduction is fused into the output
@@ -1252,7 +1270,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
 	    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) ||
-	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) || (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order))) {
+	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) || (rc = upload(s.get(), fs.qnodes, &s->ds.qnodes)) ||
+	    (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order))) {
 		rt_scene_destroy(s.release());
 		return rc;
 	}
@@ -1289,10 +1308,10 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	s->allocs.push_back(st);
 	s->stats = static_cast<unsigned long long*>(st);
 	void* fd = nullptr;
-	HIP_TRY(hipMalloc(&fd, 64));
+	HIP_TRY(hipMalloc(&fd, kFinDoneBytes));
 	s->allocs.push_back(fd);
 	s->fin_done = static_cast<uint32_t*>(fd);
-	HIP_TRY(hipMemset(s->fin_done, 0, 64));
+	HIP_TRY(hipMemset(s->fin_done, 0, kFinDoneBytes));
 	void* sm = nullptr;
 	HIP_TRY(hipMalloc(&sm, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1)));
 	s->allocs.push_back(sm);
@@ -1368,7 +1387,7 @@ void reset_after_error(rt_scene* s) {
 	}
 	(void)hipMemset(s->stats, 0, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride);
 	(void)hipMemset(s->ctr, 0, sizeof(rtamd::DeviceCounters));
-	(void)hipMemset(s->fin_done, 0, 64);
+	(void)hipMemset(s->fin_done, 0, kFinDoneBytes);
 	(void)hipDeviceSynchronize();
 	(void)hipGetLastError();
 }
@@ -1931,10 +1950,80 @@ int rt_debug_builder_digest(const rt_builder* b, uint64_t* out) {
 	vec(fs.face_geo);
 	vec(fs.face_nrm);
 	vec(fs.nodes);
+	vec(fs.qnodes);
 	vec(fs.shadow_order);
 	mix(&fs.camera, sizeof(fs.camera));
 	*out = h;
 	return RT_OK;
+}
+
+// Diagnostic (not in rtamd.h): structural check of the 4-wide trees (bvh.cpp collapse_quad)
+// against the binary LBVHs they are made from, on the host: every mesh's quad tree reaches
+// exactly the binary tree's leaves, each once, every quad child's box is the box the binary
+// tree holds for that subtree, and no path needs more than kQuadStack stack entries.
+// Returns the number of violations (0: consistent); *n_quad = quad nodes over all meshes.
+int rt_debug_quad_check(const rt_builder* b, int64_t* n_quad) {
+	if (!b) return fail(RT_ERR_ARG, "null builder");
+	const rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
+	if (n_quad) *n_quad = static_cast<int64_t>(fs.qnodes.size());
+	int bad = 0;
+	struct Leaf {
+		int32_t first, count;
+		float lo[3], hi[3];
+		bool operator<(const Leaf& o) const { return first < o.first || (first == o.first && count < o.count); }
+	};
+	for (const rtamd::DGeom& g : fs.geoms) {
+		if (g.bvh_root < 0) continue;
+		std::vector<Leaf> lb, lq;
+		std::vector<int32_t> st = {g.bvh_root};
+		while (!st.empty()) {  // binary leaves with their boxes
+			const rtamd::DBvhNode& n = fs.nodes[st.back()];
+			st.pop_back();
+			for (int c = 0; c < 2; c++) {
+				if (n.count[c] == 0) {
+					st.push_back(n.first[c]);
+					continue;
+				}
+				Leaf l{n.first[c], n.count[c], {}, {}};
+				for (int a = 0; a < 3; a++) l.lo[a] = n.lo[c][a], l.hi[a] = n.hi[c][a];
+				lb.push_back(l);
+			}
+		}
+		struct Item {
+			int32_t q, depth_push;
+		};
+		std::vector<Item> qs = {{g.qroot, 0}};
+		while (!qs.empty()) {  // quad leaves; the pushes a packet traversal could hold on the way
+			const Item it = qs.back();
+			qs.pop_back();
+			const rtamd::DQuadNode& n = fs.qnodes[it.q];
+			int inner = 0;
+			for (int c = 0; c < 4; c++) inner += n.count[c] == 0;
+			for (int c = 0; c < 4; c++) {
+				if (n.count[c] < 0) continue;
+				if (n.count[c] == 0) {
+					const int32_t pushed = it.depth_push + (inner - 1);
+					if (pushed > rtamd::kQuadStack) bad++;
+					qs.push_back({n.first[c], pushed});
+					continue;
+				}
+				Leaf l{n.first[c], n.count[c], {}, {}};
+				for (int a = 0; a < 3; a++) l.lo[a] = n.lo[a][c], l.hi[a] = n.hi[a][c];
+				lq.push_back(l);
+			}
+		}
+		std::sort(lb.begin(), lb.end());
+		std::sort(lq.begin(), lq.end());
+		if (lb.size() != lq.size()) {
+			bad++;
+			continue;
+		}
+		for (size_t k = 0; k < lb.size(); k++)
+			if (lb[k].first != lq[k].first || lb[k].count != lq[k].count ||
+			    std::memcmp(lb[k].lo, lq[k].lo, sizeof(lb[k].lo)) || std::memcmp(lb[k].hi, lq[k].hi, sizeof(lb[k].hi)))
+				bad++;
+	}
+	return bad;
 }
 
 // Diagnostic (not in rtamd.h): FETCH_SIZE calibration.  Reads a fresh `bytes` buffer once per

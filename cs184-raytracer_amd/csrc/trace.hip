@@ -34,6 +34,9 @@ __device__ __forceinline__ int64_t div_small(int64_t n, int64_t d) {
 }
 
 constexpr int kShadeBlock = 512;
+// entries of a wave-packet traversal's stack (LDS, one per wave): the quad trees need up to
+// three pushes per node
+constexpr int kWaveStack = RT_QUAD ? kQuadStack : kStackDepth;
 
 // Occupancy targets of the traversal kernels (waves per SIMD, >= 1).  4 (<= 128 VGPRs, a
 // few spills) measured 3 % faster than the compiler's 3 on C3; the wave-packet variants
@@ -420,8 +423,8 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ AppendLds append_lds;
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
 	// the traversal stacks (LBVH searches: none in a scene of spheres only)
-	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
-	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
+	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	// level records read through the constant address space (scalar loads at their uses)
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -446,19 +449,29 @@ __device__ __forceinline__ bool stat_is_max(int k) { return k == ST_MAX_BITS || 
 // The statistics reduction by the last block of a launch (FusedOut::summary): k_stats_finish's
 // work without a launch of its own.  Every block has added into the shards with device-scope
 // atomics (performed beyond the XCDs' L2s, MI355X_MICROARCH.md "Inter-workgroup
-// visibility"); each wave waits for its own to complete, the block then counts itself done on
-// one device-scope counter, and the block whose add returns the last count reduces the shards
-// (sc1 loads, L2-bypassing) into the summary (pinned host memory), clears them and the error
-// word for the next render and resets the counter.  No L2 write-back or invalidation: the
-// only data handed over are those atomics.  Every thread of the block calls it (api.cpp keeps
-// it to grids of at most 2048 blocks: one counter takes ~88 adds per us).
+// visibility"); each wave waits for its own to complete, the block then counts itself done,
+// and the block whose count completes the grid reduces the shards (sc1 loads, L2-bypassing)
+// into the summary (pinned host memory), clears them and the error word for the next render
+// and resets the counters.  No L2 write-back or invalidation: the only data handed over are
+// those atomics.  The count is sharded per XCD (blocks b with b mod 8 = x on counter x, one
+// 128-B line each; the XCD whose last block arrives adds to a top counter): one device-scope
+// counter takes only ~88 adds per us (MI355X_MICROARCH.md "dequeue").  Every thread of the
+// block calls it.
+constexpr int kFinishStride = 32;  // uint32 per counter line (128 B); FusedOut::done holds 9 lines
 __device__ void last_block_finish(unsigned long long* stats, DeviceCounters* ctr, const FusedOut& fo) {
 	__shared__ uint32_t last;
 	__shared__ unsigned long long part[kMaxWaves][ST_COUNT];
 	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's statistics atomics are performed
 	__syncthreads();
-	if (threadIdx.x == 0)
-		last = __hip_atomic_fetch_add(fo.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+	if (threadIdx.x == 0) {
+		const uint32_t nb = gridDim.x, x = blockIdx.x & 7, n_x = (nb - x + 7) / 8, n_xcd = nb < 8 ? nb : 8;
+		uint32_t* cx = fo.done + (1 + x) * kFinishStride;
+		last = 0;
+		if (__hip_atomic_fetch_add(cx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_x - 1) {
+			__hip_atomic_store(cx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every block of XCD x arrived
+			last = __hip_atomic_fetch_add(fo.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n_xcd - 1;
+		}
+	}
 	__syncthreads();
 	if (!last) return;
 	unsigned long long v[ST_COUNT];
@@ -494,7 +507,7 @@ __device__ void last_block_finish(unsigned long long* stats, DeviceCounters* ctr
 		fo.summary[t] = static_cast<unsigned long long>(
 		    __hip_atomic_load(&ctr->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 		ctr->error = 0;
-		*fo.done = 0;
+		__hip_atomic_store(fo.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 	}
 	// the summary is pinned host memory: visible at system scope before the kernel completes
 	__threadfence_system();
@@ -513,8 +526,8 @@ __global__ void __launch_bounds__(kBlock)
         DeviceScene S, FrameGeometry fg, int level, int64_t n_host, const int32_t* n_dev, int remaining, int plan_last,
         const RayLevel* levels, DeviceCounters* ctr, unsigned long long* stats, FusedOut fo) {
 	__shared__ AppendLds append_lds;
-	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
-	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
+	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
 	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur0.capacity) : n_host;
@@ -772,9 +785,9 @@ __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(!kMesh && !kPacket ? RT_SPHERE_WAVES : kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
-	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kStackDepth : kStackDepth * kBlock];
+	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
-	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kStackDepth : stack_mem + threadIdx.x;
+	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
