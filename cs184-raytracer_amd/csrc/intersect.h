@@ -867,30 +867,33 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					const bool h = slab32(cl, ch, r32, lim, tn[c]);
 					m[c] = rc[c] >= 0 ? __ballot(h) & L : 0ull;
 				}
-				// near-to-far order of the children for the wave: the entry distances of its
-				// first live lane (children that lane misses last), sorted as integers (the
-				// order of the floats); any order gives the same results
-				const int rep = static_cast<int>(__builtin_ctzll(L));
-				uint32_t key[4];
+				// closest hits: near-to-far order of the children for the wave, the entry distances
+				// of its first live lane (children that lane misses last) sorted as integers (the
+				// order of the floats), so that near faces lower the pruning limit early; the
+				// any-hit (shadow) search keeps the stored order.  Any order gives the same results.
 				int ord[4] = {0, 1, 2, 3};
+				if constexpr (!kAnyHit) {
+					const int rep = static_cast<int>(__builtin_ctzll(L));
+					uint32_t key[4];
 #pragma unroll
-				for (int c = 0; c < 4; c++) {
-					const uint32_t u = static_cast<uint32_t>(__builtin_amdgcn_readlane(__float_as_int(tn[c]), rep));
-					const bool mine = (m[c] >> rep) & 1;
-					key[c] = mine ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0xfffffff0u + c;
-				}
-				auto cswap = [&](int a, int b) {
-					if (key[ord[b]] < key[ord[a]]) {
-						const int t = ord[a];
-						ord[a] = ord[b];
-						ord[b] = t;
+					for (int c = 0; c < 4; c++) {
+						const uint32_t u = static_cast<uint32_t>(__builtin_amdgcn_readlane(__float_as_int(tn[c]), rep));
+						const bool mine = (m[c] >> rep) & 1;
+						key[c] = mine ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0xfffffff0u + c;
 					}
-				};
-				cswap(0, 1);
-				cswap(2, 3);
-				cswap(0, 2);
-				cswap(1, 3);
-				cswap(1, 2);
+					auto cswap = [&](int a, int b) {
+						if (key[ord[b]] < key[ord[a]]) {
+							const int t = ord[a];
+							ord[a] = ord[b];
+							ord[b] = t;
+						}
+					};
+					cswap(0, 1);
+					cswap(2, 3);
+					cswap(0, 2);
+					cswap(1, 3);
+					cswap(1, 2);
+				}
 				PROF_END(ws, PH_NODES, tn);
 				// inner children first, so the node to visit next is known (and its record
 				// requested) before the leaf faces are tested: the nearest inner child next, the

@@ -34,6 +34,16 @@ __device__ __forceinline__ int64_t div_small(int64_t n, int64_t d) {
 }
 
 constexpr int kShadeBlock = 512;
+typedef __attribute__((address_space(3))) double lds_f64;
+// an LDS address the compiler cannot see through: values are read back from LDS, not kept in
+// registers from the store
+__device__ __forceinline__ lds_f64* opaque_lds(lds_f64* p) {
+	asm volatile("" : "+v"(p));
+	return p;
+}
+#ifndef RT_FUSED_PARK
+#define RT_FUSED_PARK 1
+#endif
 // entries of a wave-packet traversal's stack (LDS, one per wave): the quad trees need up to
 // three pushes per node
 constexpr int kWaveStack = RT_QUAD ? kQuadStack : kStackDepth;
@@ -230,8 +240,8 @@ __device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, 
 	}
 }
 
-template <bool kPacket, bool kMesh, typename DV, typename WS>
-__device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, V3 N, DV dir_of,
+template <bool kPacket, bool kMesh, typename NV, typename DV, typename WS>
+__device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, NV n_of, DV dir_of,
                                                bool inside, int32_t* stack, DeviceCounters* ctr,
                                                unsigned long long* stats, WS& ws, double col[3]);
 
@@ -248,7 +258,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
                                              int remaining, int plan_last, const RayLevel* levels,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
                                              AppendLds& append_lds, int32_t* stack, uint32_t* stat_lds,
-                                             const FusedOut* fo = nullptr) {
+                                             const FusedOut* fo = nullptr, lds_f64* park = nullptr) {
 	// the level records (~30 buffer pointers) are read where they are used, before and after
 	// the traversal, not held in scalar registers through it
 	const int next_level = remaining > 0 ? level + 1 : level;
@@ -379,7 +389,26 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 		// miss is black (scene.cpp:66-67)
 		WorkStats<false> ws{};
 		double col[3] = {0.0, 0.0, 0.0};
-		shade_in_place<kPacket, kMesh>(S, shade, gi, P, N, [&]() { return d; }, inside, stack, ctr, stats, ws, col);
+		if constexpr (kPacket && RT_FUSED_PARK) {
+			// the shading normal and the viewing direction wait in LDS through the shadow searches
+			// (registers), read back where they are used (the per-lane form keeps them: its block's
+			// LDS, the traversal stacks, already sets its occupancy)
+			lds_f64* pk = park + threadIdx.x;
+			pk[0 * kBlock] = N.x, pk[1 * kBlock] = N.y, pk[2 * kBlock] = N.z;
+			pk[3 * kBlock] = d.x, pk[4 * kBlock] = d.y, pk[5 * kBlock] = d.z;
+			auto n_of = [&]() {
+				const lds_f64* q = opaque_lds(pk);
+				return mk(q[0 * kBlock], q[1 * kBlock], q[2 * kBlock]);
+			};
+			auto d_of = [&]() {
+				const lds_f64* q = opaque_lds(pk);
+				return mk(q[3 * kBlock], q[4 * kBlock], q[5 * kBlock]);
+			};
+			shade_in_place<kPacket, kMesh>(S, shade, gi, P, n_of, d_of, inside, stack, ctr, stats, ws, col);
+		} else {
+			shade_in_place<kPacket, kMesh>(S, shade, gi, P, [&]() { return N; }, [&]() { return d; }, inside, stack, ctr,
+			                               stats, ws, col);
+		}
 		if (!active) return;
 		if (fo->final) {
 			write_pixel(fg, i, col, true);
@@ -527,6 +556,7 @@ __global__ void __launch_bounds__(kBlock)
         const RayLevel* levels, DeviceCounters* ctr, unsigned long long* stats, FusedOut fo) {
 	__shared__ AppendLds append_lds;
 	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
+	__shared__ double park_mem[RT_FUSED_PARK && kPacket ? 6 * kBlock : 1];
 	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -539,7 +569,8 @@ __global__ void __launch_bounds__(kBlock)
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride)
 		closest_item<kPacket, false, kMesh, true>(S, fg, level, n, remaining, plan_last, levels, ctr, stats,
-		                                          base + threadIdx.x, append_lds, stack, nullptr, &fo);
+		                                          base + threadIdx.x, append_lds, stack, nullptr, &fo,
+		                                          (lds_f64*)(park_mem));
 	if (fo.summary) last_block_finish(stats, ctr, fo);
 }
 
@@ -650,14 +681,15 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 // colour is the same bits whether the light is occluded or not (it is never -0), so that ray
 // is not traced.  dv_of(): the viewing direction, read only for that test.  Every lane of
 // the wave calls it (kPacket: the search is wave-uniform; lanes without a hit pass on false).
-template <bool kPacket, bool kMesh, typename DV, typename WS>
-__device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P, V3 N, bool inside, bool zero_mat,
+template <bool kPacket, bool kMesh, typename NV, typename DV, typename WS>
+__device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P, NV n_of, bool inside, bool zero_mat,
                                               bool on, DV dv_of, int32_t* stack, DeviceCounters* ctr,
                                               unsigned long long* stats, WS& ws) {
 	V3 Ld = mk(0, 0, 1);
 	bool rev = false, zero = false;
 	double dL = 0;
 	if (on) {
+		const V3 N = n_of();
 		const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
 		const bool point = L.kind == DLIGHT_POINT;
 		const V3 lv = load3(L.vec);
@@ -692,18 +724,18 @@ __device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P,
 // A fused level's shading (closest_item<.., kFused>): the verdicts of every light for the
 // hit held in registers, then its Phong terms (scene.cpp:78-108) into col.  on: the lane has
 // a hit to shade (every lane of the wave calls it).
-template <bool kPacket, bool kMesh, typename DV, typename WS>
-__device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, V3 N, DV dir_of,
+template <bool kPacket, bool kMesh, typename NV, typename DV, typename WS>
+__device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, NV n_of, DV dir_of,
                                                bool inside, int32_t* stack, DeviceCounters* ctr,
                                                unsigned long long* stats, WS& ws, double col[3]) {
 	const bool zero_mat = on && S.mats[S.geoms[gi].mat].zero_terms;
 	unsigned long long verdicts = 0;  // bit j: the j-th non-ambient light's verdict (<= 64 lights)
 	for (int j = 0; j < S.n_nonambient; j++)
 		verdicts |= static_cast<unsigned long long>(
-		                light_verdict<kPacket, kMesh>(S, j, P, N, inside, zero_mat, on, dir_of, stack, ctr, stats, ws))
+		                light_verdict<kPacket, kMesh>(S, j, P, n_of, inside, zero_mat, on, dir_of, stack, ctr, stats, ws))
 		            << j;
 	if (on)
-		phong(S, gi, P, N, dir_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
+		phong(S, gi, P, n_of(), dir_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
 		      glibc_pow_data::kLogTab, glibc_pow_data::kExpTab, ctr, col);
 }
 
@@ -754,7 +786,7 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	}
 	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
 	for (int j = j0; j < j1; j++) {
-		const bool v = light_verdict<kPacket, kMesh>(S, j, P, N, inside, zero_mat, on, [&]() {
+		const bool v = light_verdict<kPacket, kMesh>(S, j, P, [&]() { return N; }, inside, zero_mat, on, [&]() {
 			const auto& cur = *uniform_ptr(opaque(levels) + level);
 			return mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
 		}, stack, ctr, stats, ws);
