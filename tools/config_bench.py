@@ -68,11 +68,15 @@ def main():
             s.render_device(prm, out.data_ptr(), out8.data_ptr())
             torch.cuda.synchronize()
             lat.append(time.perf_counter() - t1)
+        info = s.info()
         s.close()
         rec = {"config": name, "width": w, "height": h, "flags": flags, "ms_per_frame": round(dt * 1e3, 3),
                "frame_latency_ms": round(statistics.median(lat) * 1e3, 4),
                "rays": st.rays, "trace_rays": st.trace_rays, "shadow_rays": st.shadow_rays,
-               "Mrays_per_s": round(st.rays / dt / 1e6, 1)}
+               "Mrays_per_s": round(st.rays / dt / 1e6, 1),
+               # HBM the scene and the ray-level buffers hold after these renders (two lanes
+               # for a multi-chunk frame keep two sets of level buffers)
+               "scene_bytes": info.device_bytes, "level_bytes": info.level_bytes}
         if cli_runs > 0 and os.access(CLI, os.X_OK):
             rec["cli_wall_ms"], rec["cli_phases"] = cli_run(scene, w, h, flags, cli_runs)
         print(json.dumps(rec), flush=True)

@@ -7,16 +7,18 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kname import parse  # noqa: E402
+
 
 def load(d):
     f = [x for x in os.listdir(d) if x.endswith("counter_collection.csv")][0]
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     launches = collections.defaultdict(set)
     for r in csv.DictReader(open(os.path.join(d, f))):
-        m = re.search(r"k_\w+(<[\w, ]+>)?", r["Kernel_Name"])
-        if not m or m.group(0).endswith(", true>"):  # counting instantiations (bench.py solo pass)
+        k = parse(r["Kernel_Name"])[1]
+        if not k:  # counting instantiations (bench.py solo pass)
             continue
-        k = m.group(0).replace(", false>", ">")
         per[k][r["Counter_Name"]] += float(r["Counter_Value"])
         launches[k].add(r["Dispatch_Id"])
     return per, {k: len(v) for k, v in launches.items()}

@@ -20,16 +20,15 @@ import re
 import shutil
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kname import parse  # noqa: E402
+
 CALIB_BYTES = 1 << 30
 
 
 def family(name):
-    """Kernel family; None for the counting instantiations (<..., true>: bench.py's solo pass
-    makes one counting call for the work counts, the roofline times the other)."""
-    m = re.search(r"(k_[a-z0-9_]+)(<[^>]*>)?\(", name)
-    if not m or (m.group(2) and m.group(2).endswith(", true>")):
-        return None
-    return m.group(1)
+    """Kernel family; None for the counting instantiations (tools/kname.py)."""
+    return parse(name)[0]
 
 
 def per_dispatch(path, counter):

@@ -24,16 +24,15 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kname import parse  # noqa: E402
+
 N_XCD, N_CU, N_SIMD = 8, 256, 1024
 
 
 def variant(name):
-    """k_shadow<true> etc.; None for the counting instantiations (<..., true>: bench.py's solo
-    pass makes one counting call for the work counts, the roofline times the other)."""
-    m = re.search(r"(k_[a-z0-9_]+(?:<[^>]*>)?)\(", name)
-    if not m or m.group(1).endswith(", true>"):
-        return None
-    return m.group(1).replace("(anonymous namespace)::", "").replace(", false>", ">")
+    """k_shadow<true, true> etc. (tools/kname.py); None for the counting instantiations."""
+    return parse(name)[1]
 
 
 def family(v):
