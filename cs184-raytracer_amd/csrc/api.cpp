@@ -173,6 +173,21 @@ struct Lane {
 	rtamd::ChunkRow* rows_pin = nullptr;  // its pinned staging (one chunk in flight per lane)
 	int64_t rows_cap = 0;
 	int64_t rows_uploaded = -1;           // rows of the table now on the device (-1: none), = rows_pin[0, n)
+	// row tables already on the device, by content (launch plans issued directly, RTAMD_GRAPH 2):
+	// a chunk whose table is among them needs no upload (an H2D copy from pinned memory is a blit
+	// kernel of 30-50 us on the chain's critical path); the lanes of a multi-chunk frame or of a
+	// batch alternate between a few tables
+	struct RowTable {
+		std::vector<rtamd::ChunkRow> host;  // the content (exact comparison)
+		uint64_t hash = 0;
+		rtamd::ChunkRow* dev = nullptr;
+		int64_t cap = 0;
+		uint64_t used = 0;
+	};
+	std::vector<RowTable> tables;
+	uint64_t table_clock = 0;
+	RowTable* table_pending = nullptr;    // the table the current chunk's rows are being copied into
+	uint64_t table_pending_hash = 0;
 	int level = 0;                        // the level whose counts are awaited
 	std::vector<int64_t> level_n;         // ray counts of the levels known so far
 	std::vector<int> shaded;                        // first level of each shading launch
@@ -414,6 +429,8 @@ void lane_destroy(Lane& ln) {
 	clear_plans(ln);
 	if (ln.rows_dev) (void)hipFree(ln.rows_dev);
 	if (ln.rows_pin) (void)hipHostFree(ln.rows_pin);
+	for (auto& t : ln.tables)
+		if (t.dev) (void)hipFree(t.dev);
 	for (auto& L : ln.levels)
 		if (L.block) (void)hipFree(L.block);
 	if (ln.levels_pinned) (void)hipHostFree(ln.levels_pinned);
@@ -840,6 +857,47 @@ struct Render {
 		ln.rows_hash = h;
 		*copy = !same;
 		ln.rows_uploaded = n_rows;
+		ln.fg.rows = ln.rows_dev;
+		if (s->graphs == 1) return RT_OK;  // captured graphs hold the one table's address
+		// the content's table among the lane's cached ones, else a new (or the least recently
+		// used) one takes it; *copy then says whether that table must be uploaded
+		uint64_t hc = 1469598103934665603ull;
+		const unsigned char* bytes = reinterpret_cast<const unsigned char*>(ln.rows_pin);
+		for (int64_t k = 0; k < n_rows * static_cast<int64_t>(sizeof(rtamd::ChunkRow)); k++)
+			hc = (hc ^ bytes[k]) * 1099511628211ull;
+		constexpr size_t kMaxTables = 64;
+		ln.tables.reserve(kMaxTables);  // table_pending points into it: never reallocated
+		ln.table_pending = nullptr;
+		Lane::RowTable* t = nullptr;
+		for (auto& c : ln.tables)
+			if (c.hash == hc && static_cast<int64_t>(c.host.size()) == n_rows &&
+			    std::memcmp(c.host.data(), ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow)) == 0)
+				t = &c;
+		*copy = t == nullptr;
+		if (!t) {
+			if (ln.tables.size() < kMaxTables) {
+				ln.tables.emplace_back();
+				t = &ln.tables.back();
+			} else {
+				t = &*std::min_element(ln.tables.begin(), ln.tables.end(),
+				                       [](const Lane::RowTable& a, const Lane::RowTable& b) { return a.used < b.used; });
+			}
+			if (t->cap < n_rows) {
+				if (t->dev) HIP_TRY(hipFree(t->dev));
+				t->dev = nullptr;
+				t->cap = 0;
+				HIP_TRY(hipMalloc(reinterpret_cast<void**>(&t->dev), std::max<int64_t>(n_rows, 64) * sizeof(rtamd::ChunkRow)));
+				t->cap = std::max<int64_t>(n_rows, 64);
+			}
+			// valid only once its upload is queued (start_chunk commits it)
+			t->host.clear();
+			t->hash = 0;
+			ln.table_pending = t;
+			ln.table_pending_hash = hc;
+		}
+		t->used = ++ln.table_clock;
+		ln.fg.rows = t->dev;
+		ln.rows_uploaded = -1;  // rows_dev is not the chunk's table
 		return RT_OK;
 	}
 
@@ -855,11 +913,12 @@ struct Render {
 		bool copy_rows = false;
 		int rc = prepare_rows(ln, segs, n_rows, &copy_rows);
 		if (rc) return rc;
+		const rtamd::ChunkRow* rows = ln.fg.rows;  // prepare_rows: the chunk's row table
 		ln.fg = rtamd::FrameGeometry{};
 		ln.fg.width = first.p->width;
 		ln.fg.height = first.p->height;
 		ln.fg.intersection_only = first.io;
-		ln.fg.rows = ln.rows_dev;
+		ln.fg.rows = rows;
 		ln.level = 0;
 		ln.level_n.assign(1, ln.n0);
 		ln.shaded.clear();
@@ -873,7 +932,13 @@ struct Render {
 		const hipStream_t st = ln.direct ? caller : ln.stream;
 		if (!ln.direct && (rc = fork(ln))) return rc;
 		if (copy_rows)
-			HIP_TRY(hipMemcpyAsync(ln.rows_dev, ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow), hipMemcpyHostToDevice, st));
+			HIP_TRY(hipMemcpyAsync(const_cast<rtamd::ChunkRow*>(ln.fg.rows), ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow),
+			                       hipMemcpyHostToDevice, st));
+		if (ln.table_pending) {  // its upload is queued ahead of every kernel that reads it
+			ln.table_pending->host.assign(ln.rows_pin, ln.rows_pin + n_rows);
+			ln.table_pending->hash = ln.table_pending_hash;
+			ln.table_pending = nullptr;
+		}
 		if (!pl && (pl = adopt_plan(ln, key_of(ln), rc), rc)) return rc;
 		if (pl) {
 			if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
@@ -1378,6 +1443,11 @@ void reset_after_error(rt_scene* s) {
 		ln->phase = Lane::IDLE;
 		ln->segs.clear();
 		ln->rows_uploaded = -1;
+		ln->table_pending = nullptr;
+		for (auto& t : ln->tables) {  // forget the cached contents (an upload may have failed)
+			t.host.clear();
+			t.hash = 0;
+		}
 		ln->level = 0;
 		ln->level_n.clear();
 		ln->shaded.clear();
