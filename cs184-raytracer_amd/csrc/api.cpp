@@ -272,6 +272,7 @@ struct rt_scene {
 	// hits + shadow rays + Phong terms, and for a plan of one level the output pixels too)
 	// instead of k_closest + k_shadow (+ k_shade) per level and k_output
 	int fused = 1;
+	int fuse_level0 = 0;  // RTAMD_FUSE_LEVEL0: level 0 of a multi-stream replay as one k_fused (1: calls of several chunks, 2: always)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
 	// (no fork/join across queues) and its last kernel finishes the statistics (no
 	// k_stats_finish launch)
@@ -701,19 +702,27 @@ struct Render {
 				launches[2] += scratch.launches[2];
 			}
 		} else {
+			const bool fuse0 = fusable(ln) && (s->fuse_level0 == 2 || (s->fuse_level0 == 1 && !direct_ok));
 			for (int L = 0; L < nlev && rc == RT_OK; L++) {
 				const int remaining = depth - L;
 				const bool last = L == nlev - 1;
 				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
-				step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
-				                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
-				                           last && remaining > 0));
+				// level 0 fused (closest, shadow searches and Phong in one launch): its shading
+				// joins the chain instead of running beside it (a throughput trade for batches)
+				const bool fuse = L == 0 && fuse0;
+				if (fuse)
+					step(rtamd::launch_fused(s->ds, ln.fg, L, bound, nullptr, remaining, ln.levels_dev, s->ctr, s->stats, st,
+					                         s->packet_mask, last && remaining > 0, rtamd::FusedOut{}));
+				else
+					step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
+					                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
+					                           last && remaining > 0));
 				launches[0]++;
 				hipEvent_t done = ev(L, 1);
 				step(done ? hipEventRecord(done, st) : hipErrorOutOfMemory);
 				// shading beside the chain only where a later level's tracing can overlap it: a
 				// wait on a not yet signalled event of another queue costs tens of microseconds
-				if (L < direct_levels && rc == RT_OK) {
+				if (L < direct_levels && !fuse && rc == RT_OK) {
 					const bool side = L < nlev - 1;
 					hipStream_t q = side ? shade_stream(ln, L % 3) : st;
 					if (!q) step(hipErrorOutOfMemory);
@@ -1319,6 +1328,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* os = std::getenv("RTAMD_ONE_STREAM_PIXELS")) s->one_stream_pixels = std::atoll(os);
 	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
+	if (const char* f0 = std::getenv("RTAMD_FUSE_LEVEL0")) s->fuse_level0 = std::atoi(f0);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
