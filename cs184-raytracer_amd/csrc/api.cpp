@@ -272,7 +272,8 @@ struct rt_scene {
 	// hits + shadow rays + Phong terms, and for a plan of one level the output pixels too)
 	// instead of k_closest + k_shadow (+ k_shade) per level and k_output
 	int fused = 1;
-	int fuse_level0 = 0;  // RTAMD_FUSE_LEVEL0: level 0 of a multi-stream replay as one k_fused (1: calls of several chunks, 2: always)
+	int fuse_level0 = 0;
+	int fuse_last = 0;    // RTAMD_FUSE_LAST: the last level of a multi-stream replay as one k_fused (its shading is on the chain's tail anyway)  // RTAMD_FUSE_LEVEL0: level 0 of a multi-stream replay as one k_fused (1: calls of several chunks, 2: always)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
 	// (no fork/join across queues) and its last kernel finishes the statistics (no
 	// k_stats_finish launch)
@@ -703,15 +704,17 @@ struct Render {
 			}
 		} else {
 			const bool fuse0 = fusable(ln) && (s->fuse_level0 == 2 || (s->fuse_level0 == 1 && !direct_ok));
+			const bool fuse_tail = fusable(ln) && s->fuse_last && nlev > 1;
 			for (int L = 0; L < nlev && rc == RT_OK; L++) {
 				const int remaining = depth - L;
 				const bool last = L == nlev - 1;
 				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
 				// level 0 fused (closest, shadow searches and Phong in one launch): its shading
 				// joins the chain instead of running beside it (a throughput trade for batches)
-				const bool fuse = L == 0 && fuse0;
+				const bool fuse = (L == 0 && fuse0) || (last && fuse_tail);
 				if (fuse)
-					step(rtamd::launch_fused(s->ds, ln.fg, L, bound, nullptr, remaining, ln.levels_dev, s->ctr, s->stats, st,
+					step(rtamd::launch_fused(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
+					                         remaining, ln.levels_dev, s->ctr, s->stats, st,
 					                         s->packet_mask, last && remaining > 0, rtamd::FusedOut{}));
 				else
 					step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
@@ -739,10 +742,10 @@ struct Render {
 				}
 			}
 			// the deep levels after the chain, on its own stream (the reductions wait for them)
-			if (rc == RT_OK && nlev > direct_levels) {
+			if (rc == RT_OK && nlev - (fuse_tail ? 1 : 0) > direct_levels) {
 				hipStream_t q = st;
 				std::vector<int> deep;
-				for (int L = direct_levels; L < nlev; L++) deep.push_back(L);
+				for (int L = direct_levels; L < nlev - (fuse_tail ? 1 : 0); L++) deep.push_back(L);
 				for (size_t k = 0, e; k < deep.size() && rc == RT_OK; k = e) {
 					e = std::min(deep.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
 					scratch.launches[1] = scratch.launches[2] = 0;
@@ -1329,6 +1332,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
 	if (const char* f0 = std::getenv("RTAMD_FUSE_LEVEL0")) s->fuse_level0 = std::atoi(f0);
+	if (const char* fl = std::getenv("RTAMD_FUSE_LAST")) s->fuse_last = std::atoi(fl);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
