@@ -101,10 +101,14 @@ _W, _H = (int(v) for v in os.environ.get("RTAMD_FUZZ_SIZE", "56x40").split("x"))
 
 @pytest.mark.parametrize("seed", range(_BASE, _BASE + _SEEDS))
 def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
-    # odd seeds: the production light-major threshold (every launch here is below it)
-    monkeypatch.setenv("RTAMD_LIGHT_MAJOR_BELOW", "131072" if seed % 2 else "0")
-    monkeypatch.setenv("RTAMD_ONE_STREAM_PIXELS", "131072" if seed % 2 else "0")
-    monkeypatch.setenv("RTAMD_ONE_STREAM_LEVEL1", "1" if seed % 2 else "0")
+    # odd seeds: the production light-major threshold (every launch here is below it);
+    # RTAMD_FUZZ_PRODUCTION=1: every seed under the library's own defaults (and rendered twice)
+    production = seed % 2 or os.environ.get("RTAMD_FUZZ_PRODUCTION") == "1"
+    for knob in ("RTAMD_LIGHT_MAJOR_BELOW", "RTAMD_ONE_STREAM_PIXELS", "RTAMD_ONE_STREAM_LEVEL1"):
+        if production:
+            monkeypatch.delenv(knob, raising=False)
+        else:
+            monkeypatch.setenv(knob, "0")
     path, bdepth, io = random_scene(seed, tmp_path)
     w, h = _W, _H
     try:
@@ -121,7 +125,7 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
     opts = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth, intersectionOnly_=io)
     got = s.renderScene(options=opts)
     st = s.last_stats
-    if seed % 2:  # again: the first render traced host-driven and built a launch plan; this one replays it
+    if production:  # again: the first render traced host-driven and built a launch plan; this one replays it
         again = s.renderScene(options=opts)
         assert np.array_equal(np.ascontiguousarray(again).view(np.uint64), np.ascontiguousarray(got).view(np.uint64))
         assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (st.trace_rays, st.shadow_rays)
