@@ -2,7 +2,7 @@
 variants (each variant in its own process, since the library reads its knobs at scene
 creation), rounds alternating on one box.
 
-usage: python tools/latency_ab.py <rounds> <config[,config...]> [VAR=V[,VAR=V]] ...
+usage: python tools/latency_ab.py <rounds> <config[@k/n][,config...]> [VAR=V[,VAR=V]] ...
        (the first variant is always the default environment)"""
 import json
 import os
@@ -19,12 +19,16 @@ import torch, rtamd
 from rtamd.configs import CONFIGS, SCENES, option_kwargs
 res = {}
 for name in sys.argv[1].split(","):
-    scene, w, h, flags = CONFIGS[name]
+    cfg, _, share = name.partition("@")
+    scene, w, h, flags = CONFIGS[cfg]
     kw = option_kwargs(flags)
     s = rtamd.load_scene(os.path.join(SCENES, scene))
     out = torch.empty((h, w, 3), dtype=torch.float64, device="cuda")
     out8 = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
     prm = s.params(w, h, kw["bdepth"], kw["intersection_only"], 0, h, 1)
+    if share:  # rank k's 8-row-block share of an n-way partition (bench.py's strong-scaling sweep)
+        k, n = (int(v) for v in share.split("/"))
+        prm = s.params(w, h, kw["bdepth"], kw["intersection_only"], k * 8, h, n, row_block=8)
     reps = int(sys.argv[2])
     ts = []
     for i in range(reps + 5):
