@@ -272,6 +272,7 @@ struct rt_scene {
 	// hits + shadow rays + Phong terms, and for a plan of one level the output pixels too)
 	// instead of k_closest + k_shadow (+ k_shade) per level and k_output
 	int fused = 1;
+	int64_t fused_min_pixels = 0;
 	int fuse_level0 = 0;
 	int fuse_last = 0;    // RTAMD_FUSE_LAST: the last level of a multi-stream replay as one k_fused (its shading is on the chain's tail anyway)  // RTAMD_FUSE_LEVEL0: level 0 of a multi-stream replay as one k_fused (1: calls of several chunks, 2: always)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
@@ -488,8 +489,10 @@ struct Render {
 	}
 	// its levels are fused launches (k_fused): shaded renders of at most 64 shadow lights,
 	// without the work counters
+	// (RTAMD_FUSED_MIN_PIXELS: a mesh scene's chunk of fewer pixels keeps the split launches)
 	bool fusable(const Lane& ln) const {
-		return s->fused && !ln.io && !s->ds.work_stats && s->ds.n_nonambient <= rtamd::kMaxShadowLights;
+		return s->fused && !ln.io && !s->ds.work_stats && s->ds.n_nonambient <= rtamd::kMaxShadowLights &&
+		       (s->ds.n_meshes == 0 || ln.n0 >= s->fused_min_pixels);
 	}
 
 	// k_closest of level L, then the read-back of its counts.  n: the level's ray count, or
@@ -1332,6 +1335,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
 	if (const char* f0 = std::getenv("RTAMD_FUSE_LEVEL0")) s->fuse_level0 = std::atoi(f0);
+	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
 	if (const char* fl = std::getenv("RTAMD_FUSE_LAST")) s->fuse_last = std::atoi(fl);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
