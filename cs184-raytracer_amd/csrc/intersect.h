@@ -804,6 +804,10 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 #ifndef RT_QUAD
 #define RT_QUAD 1
 #endif
+// RT_QUAD_PREFETCH: the next quad node's record is requested before the leaf faces are tested
+#ifndef RT_QUAD_PREFETCH
+#define RT_QUAD_PREFETCH 1
+#endif
 // A value every lane holds equally (node and face indices of the packet traversal): read
 // from the first lane, so the compiler keeps it in an SGPR and the node/face records at
 // that index are fetched with scalar loads instead of 64 identical vector loads.
@@ -921,7 +925,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					lt[k] = tn[c];
 				}
 				if (next < 0 && sp > 0) next = uniform_i32(wstack[--sp]);
-				if (next >= 0) fetch(next);
+				if (RT_QUAD_PREFETCH && next >= 0) fetch(next);
 				// each later leaf is tested again against the limit the earlier ones' faces may
 				// have lowered
 				bool tested = false;
@@ -944,6 +948,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					PROF_END(ws, PH_FACES, tf);
 				}
 				if (next < 0 || !wave_any(live)) break;
+				if (!RT_QUAD_PREFETCH) fetch(next);
 			}
 		} else if (!(RT_DIAG_SKIP & 1)) {
 			ws.add(W_ENTRIES, live);
