@@ -272,9 +272,12 @@ struct rt_scene {
 	// hits + shadow rays + Phong terms, and for a plan of one level the output pixels too)
 	// instead of k_closest + k_shadow (+ k_shade) per level and k_output
 	int fused = 1;
-	int64_t fused_min_pixels = 0;
-	int fuse_level0 = 0;
-	int fuse_last = 0;    // RTAMD_FUSE_LAST: the last level of a multi-stream replay as one k_fused (its shading is on the chain's tail anyway)  // RTAMD_FUSE_LEVEL0: level 0 of a multi-stream replay as one k_fused (1: calls of several chunks, 2: always)
+	// RTAMD_FUSED_MIN_PIXELS: a mesh scene's chunk of fewer pixels keeps the split launches.  Such
+	// a chunk is one round of waves, so its time is its slowest tile's; fused, that tile also
+	// traces every light's shadow rays in turn, split the shadow rays are spread over a second
+	// launch of (hit, light) items: the C4 1/8 row share 0.234 -> 0.208 ms, C1-C4 unchanged
+	// (profiles/round4/ab/latency_quad_fuse_knobs.txt)
+	int64_t fused_min_pixels = 524288;
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
 	// (no fork/join across queues) and its last kernel finishes the statistics (no
 	// k_stats_finish launch)
@@ -489,7 +492,7 @@ struct Render {
 	}
 	// its levels are fused launches (k_fused): shaded renders of at most 64 shadow lights,
 	// without the work counters
-	// (RTAMD_FUSED_MIN_PIXELS: a mesh scene's chunk of fewer pixels keeps the split launches)
+	// (rt_scene::fused_min_pixels: not a small chunk of a mesh scene)
 	bool fusable(const Lane& ln) const {
 		return s->fused && !ln.io && !s->ds.work_stats && s->ds.n_nonambient <= rtamd::kMaxShadowLights &&
 		       (s->ds.n_meshes == 0 || ln.n0 >= s->fused_min_pixels);
@@ -706,29 +709,19 @@ struct Render {
 				launches[2] += scratch.launches[2];
 			}
 		} else {
-			const bool fuse0 = fusable(ln) && (s->fuse_level0 == 2 || (s->fuse_level0 == 1 && !direct_ok));
-			const bool fuse_tail = fusable(ln) && s->fuse_last && nlev > 1;
 			for (int L = 0; L < nlev && rc == RT_OK; L++) {
 				const int remaining = depth - L;
 				const bool last = L == nlev - 1;
 				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
-				// level 0 fused (closest, shadow searches and Phong in one launch): its shading
-				// joins the chain instead of running beside it (a throughput trade for batches)
-				const bool fuse = (L == 0 && fuse0) || (last && fuse_tail);
-				if (fuse)
-					step(rtamd::launch_fused(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
-					                         remaining, ln.levels_dev, s->ctr, s->stats, st,
-					                         s->packet_mask, last && remaining > 0, rtamd::FusedOut{}));
-				else
-					step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
-					                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
-					                           last && remaining > 0));
+				step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
+				                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
+				                           last && remaining > 0));
 				launches[0]++;
 				hipEvent_t done = ev(L, 1);
 				step(done ? hipEventRecord(done, st) : hipErrorOutOfMemory);
 				// shading beside the chain only where a later level's tracing can overlap it: a
 				// wait on a not yet signalled event of another queue costs tens of microseconds
-				if (L < direct_levels && !fuse && rc == RT_OK) {
+				if (L < direct_levels && rc == RT_OK) {
 					const bool side = L < nlev - 1;
 					hipStream_t q = side ? shade_stream(ln, L % 3) : st;
 					if (!q) step(hipErrorOutOfMemory);
@@ -745,10 +738,10 @@ struct Render {
 				}
 			}
 			// the deep levels after the chain, on its own stream (the reductions wait for them)
-			if (rc == RT_OK && nlev - (fuse_tail ? 1 : 0) > direct_levels) {
+			if (rc == RT_OK && nlev > direct_levels) {
 				hipStream_t q = st;
 				std::vector<int> deep;
-				for (int L = direct_levels; L < nlev - (fuse_tail ? 1 : 0); L++) deep.push_back(L);
+				for (int L = direct_levels; L < nlev; L++) deep.push_back(L);
 				for (size_t k = 0, e; k < deep.size() && rc == RT_OK; k = e) {
 					e = std::min(deep.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
 					scratch.launches[1] = scratch.launches[2] = 0;
@@ -1334,9 +1327,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* os = std::getenv("RTAMD_ONE_STREAM_PIXELS")) s->one_stream_pixels = std::atoll(os);
 	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
-	if (const char* f0 = std::getenv("RTAMD_FUSE_LEVEL0")) s->fuse_level0 = std::atoi(f0);
 	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
-	if (const char* fl = std::getenv("RTAMD_FUSE_LAST")) s->fuse_last = std::atoi(fl);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
@@ -1353,7 +1344,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
 	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
 	    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) ||
-	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) || (rc = upload(s.get(), fs.qnodes, &s->ds.qnodes)) ||
+	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) ||
 	    (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order))) {
 		rt_scene_destroy(s.release());
 		return rc;
@@ -2038,80 +2029,10 @@ int rt_debug_builder_digest(const rt_builder* b, uint64_t* out) {
 	vec(fs.face_geo);
 	vec(fs.face_nrm);
 	vec(fs.nodes);
-	vec(fs.qnodes);
 	vec(fs.shadow_order);
 	mix(&fs.camera, sizeof(fs.camera));
 	*out = h;
 	return RT_OK;
-}
-
-// Diagnostic (not in rtamd.h): structural check of the 4-wide trees (bvh.cpp collapse_quad)
-// against the binary LBVHs they are made from, on the host: every mesh's quad tree reaches
-// exactly the binary tree's leaves, each once, every quad child's box is the box the binary
-// tree holds for that subtree, and no path needs more than kQuadStack stack entries.
-// Returns the number of violations (0: consistent); *n_quad = quad nodes over all meshes.
-int rt_debug_quad_check(const rt_builder* b, int64_t* n_quad) {
-	if (!b) return fail(RT_ERR_ARG, "null builder");
-	const rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
-	if (n_quad) *n_quad = static_cast<int64_t>(fs.qnodes.size());
-	int bad = 0;
-	struct Leaf {
-		int32_t first, count;
-		float lo[3], hi[3];
-		bool operator<(const Leaf& o) const { return first < o.first || (first == o.first && count < o.count); }
-	};
-	for (const rtamd::DGeom& g : fs.geoms) {
-		if (g.bvh_root < 0) continue;
-		std::vector<Leaf> lb, lq;
-		std::vector<int32_t> st = {g.bvh_root};
-		while (!st.empty()) {  // binary leaves with their boxes
-			const rtamd::DBvhNode& n = fs.nodes[st.back()];
-			st.pop_back();
-			for (int c = 0; c < 2; c++) {
-				if (n.count[c] == 0) {
-					st.push_back(n.first[c]);
-					continue;
-				}
-				Leaf l{n.first[c], n.count[c], {}, {}};
-				for (int a = 0; a < 3; a++) l.lo[a] = n.lo[c][a], l.hi[a] = n.hi[c][a];
-				lb.push_back(l);
-			}
-		}
-		struct Item {
-			int32_t q, depth_push;
-		};
-		std::vector<Item> qs = {{g.qroot, 0}};
-		while (!qs.empty()) {  // quad leaves; the pushes a packet traversal could hold on the way
-			const Item it = qs.back();
-			qs.pop_back();
-			const rtamd::DQuadNode& n = fs.qnodes[it.q];
-			int inner = 0;
-			for (int c = 0; c < 4; c++) inner += n.count[c] == 0;
-			for (int c = 0; c < 4; c++) {
-				if (n.count[c] < 0) continue;
-				if (n.count[c] == 0) {
-					const int32_t pushed = it.depth_push + (inner - 1);
-					if (pushed > rtamd::kQuadStack) bad++;
-					qs.push_back({n.first[c], pushed});
-					continue;
-				}
-				Leaf l{n.first[c], n.count[c], {}, {}};
-				for (int a = 0; a < 3; a++) l.lo[a] = n.lo[a][c], l.hi[a] = n.hi[a][c];
-				lq.push_back(l);
-			}
-		}
-		std::sort(lb.begin(), lb.end());
-		std::sort(lq.begin(), lq.end());
-		if (lb.size() != lq.size()) {
-			bad++;
-			continue;
-		}
-		for (size_t k = 0; k < lb.size(); k++)
-			if (lb[k].first != lq[k].first || lb[k].count != lq[k].count ||
-			    std::memcmp(lb[k].lo, lq[k].lo, sizeof(lb[k].lo)) || std::memcmp(lb[k].hi, lq[k].hi, sizeof(lb[k].hi)))
-				bad++;
-	}
-	return bad;
 }
 
 // Diagnostic (not in rtamd.h): FETCH_SIZE calibration.  Reads a fresh `bytes` buffer once per

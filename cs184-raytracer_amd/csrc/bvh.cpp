@@ -185,71 +185,6 @@ struct Builder {
 	}
 };
 
-// The 4-wide tree of a binary LBVH (DQuadNode, the packet traversal): a quad node takes the
-// two children of a binary node and, while it has fewer than four, replaces the inner child
-// of largest box area by that node's two children.  Every child keeps the padded fp32 box
-// its binary parent held for it, so the quad traversal tests the same boxes (conservative
-// by the same margin) and reaches the same leaves; only the grouping of the node fetches
-// changes.  Depth-first order (a node's first child follows it).  Returns the root's index.
-int32_t collapse_quad(const std::vector<DBvhNode>& bin, int32_t b, std::vector<DQuadNode>& q) {
-	struct Child {
-		float lo[3], hi[3];
-		int32_t first, count;
-	};
-	auto child_of = [&](int32_t n, int c) {
-		Child r;
-		for (int a = 0; a < 3; a++) {
-			r.lo[a] = bin[n].lo[c][a];
-			r.hi[a] = bin[n].hi[c][a];
-		}
-		r.first = bin[n].first[c];
-		r.count = bin[n].count[c];
-		return r;
-	};
-	auto area = [](const Child& c) {
-		const double x = static_cast<double>(c.hi[0]) - c.lo[0], y = static_cast<double>(c.hi[1]) - c.lo[1],
-		             z = static_cast<double>(c.hi[2]) - c.lo[2];
-		return x * y + y * z + z * x;
-	};
-	std::vector<Child> ch = {child_of(b, 0), child_of(b, 1)};
-	while (ch.size() < 4) {
-		int best = -1;
-		double best_area = -1;
-		for (size_t k = 0; k < ch.size(); k++)
-			if (ch[k].count == 0 && area(ch[k]) > best_area) {
-				best_area = area(ch[k]);
-				best = static_cast<int>(k);
-			}
-		if (best < 0) break;
-		const int32_t n = ch[best].first;
-		ch[best] = child_of(n, 0);
-		ch.insert(ch.begin() + best + 1, child_of(n, 1));
-	}
-	const int32_t idx = static_cast<int32_t>(q.size());
-	q.emplace_back();
-	DQuadNode out;
-	std::memset(&out, 0, sizeof(out));
-	for (int c = 0; c < 4; c++) {
-		if (c >= static_cast<int>(ch.size())) {
-			for (int a = 0; a < 3; a++) {
-				out.lo[a][c] = INFINITY;
-				out.hi[a][c] = -INFINITY;
-			}
-			out.first[c] = 0;
-			out.count[c] = -1;
-			continue;
-		}
-		for (int a = 0; a < 3; a++) {
-			out.lo[a][c] = ch[c].lo[a];
-			out.hi[a][c] = ch[c].hi[a];
-		}
-		out.count[c] = ch[c].count;
-		out.first[c] = ch[c].count > 0 ? ch[c].first : collapse_quad(bin, ch[c].first, q);
-	}
-	q[idx] = out;
-	return idx;
-}
-
 // Padded world-space box of an object-space box (the eight corners through fwd).  Used
 // only to skip geometries a ray cannot hit; a degenerate transform disables it.
 void world_box(const Geometry& g, const double lo[3], const double hi[3], DGeom& d) {
@@ -373,7 +308,6 @@ FlatScene flatten_scene(const Scene& s) {
 		d.kind = g.kind;
 		d.flip = g.det < 0;
 		d.bvh_root = -1;
-		d.qroot = -1;
 		d.may_raise = direction_may_vanish(g.inv);
 		fs.n_may_raise += d.may_raise;
 		DMaterial m;
@@ -507,7 +441,6 @@ FlatScene flatten_scene(const Scene& s) {
 			break;
 		}
 		d.bvh_root = static_cast<int32_t>(node_base);
-		d.qroot = collapse_quad(fs.nodes, d.bvh_root, fs.qnodes);
 		fs.geoms.push_back(d);
 	}
 	// shadow-test order: spheres and linear meshes first, then BVH meshes by size

@@ -16,7 +16,6 @@ struct FlatScene {
 	std::vector<DFaceGeo> face_geo;
 	std::vector<DFaceNrm> face_nrm;
 	std::vector<DBvhNode> nodes;
-	std::vector<DQuadNode> qnodes;  // the same trees, 4-wide (packet traversal)
 	// geometry indices in shadow-test order: the occlusion query is an `any` over the
 	// geometries, so cheap ones (spheres, linearly scanned meshes) go first
 	std::vector<int32_t> shadow_order;

@@ -45,10 +45,7 @@ struct alignas(16) DGeom {
 	// "ray has no direction" (rtbase.h:17-23): every ray must then check this geometry,
 	// even where culling or an early exit would skip it (bvh.cpp, intersect.h).
 	int32_t may_raise;
-	int32_t qroot;        // root of the mesh's 4-wide tree (DQuadNode, the packet traversal), -1 = none
-	int32_t pad[2];
 };
-static_assert(sizeof(DGeom) == 368, "geometry record: 368 B");
 
 struct alignas(16) DMaterial {   // rtbase.h:30-39
 	double ka[3], kd[3], ks[3], kr[3], kt[3];
@@ -98,21 +95,6 @@ struct alignas(64) DBvhNode {
 	int32_t count[2];
 };
 
-// The 4-wide form of a mesh's LBVH for the wave-packet traversal (bvh.cpp collapse_quad):
-// every node holds up to four children of the binary tree, each with the same padded fp32 box
-// the binary parent held for it, so one scalar fetch (two 64-B loads) brings four child boxes
-// and the chain of dependent node fetches is about half as long.  Child c: leaf when
-// count[c] > 0 (faces [first[c], first[c] + count[c]) of the mesh), inner quad node first[c]
-// when count[c] == 0, no child when count[c] < 0.
-struct alignas(128) DQuadNode {
-	float lo[3][4], hi[3][4];  // [axis][child]
-	int32_t first[4];
-	int32_t count[4];
-};
-static_assert(sizeof(DQuadNode) == 128, "quad node: 128 B");
-// stack entries per wave of the quad packet traversal: at most 3 pushes per node on a path of
-// at most kStackDepth - 2 nodes (the binary tree's depth bound, bvh.cpp)
-constexpr int kQuadStack = 3 * (RT_STACK_DEPTH - 2);
 
 struct DCamera {
 	double eye[4], ll[4], lr[4], ul[4], ur[4];

@@ -800,14 +800,6 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 // test there (pruning and tie-breaks are per lane), it may only test a few more.
 // Callers must reach these functions with all lanes (inactive lanes pass on = false).
 
-// RT_QUAD: the packet traversal walks the 4-wide trees (DQuadNode); 0: the binary LBVH
-#ifndef RT_QUAD
-#define RT_QUAD 1
-#endif
-// RT_QUAD_PREFETCH: the next quad node's record is requested before the leaf faces are tested
-#ifndef RT_QUAD_PREFETCH
-#define RT_QUAD_PREFETCH 1
-#endif
 // A value every lane holds equally (node and face indices of the packet traversal): read
 // from the first lane, so the compiler keeps it in an SGPR and the node/face records at
 // that index are fetched with scalar loads instead of 64 identical vector loads.
@@ -834,122 +826,6 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				live = live && !hitf;
 			}
 				PROF_END(ws, PH_FACES, tf);
-		} else if (!(RT_DIAG_SKIP & 1) && RT_QUAD) {
-			ws.add(W_ENTRIES, live);
-			const V3 inv = safe_inv(d);
-			const Ray32 r32 = ray32(G, o, d, inv);
-			float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);  // changes only with best.dist
-			const auto qn = uniform_ptr(S.qnodes);
-			const int32_t fbase = uniform_i32(G->face_begin);
-			int sp = 0;
-			// the quad node record (128 B, two scalar loads): four child boxes tested by every
-			// lane (a lane that is done ignores its results)
-			float lo[3][4], hi[3][4];
-			int32_t rf[4], rc[4];
-			auto fetch = [&](int32_t n) {
-				const auto N = qn + n;
-#pragma unroll
-				for (int a = 0; a < 3; a++)
-#pragma unroll
-					for (int c = 0; c < 4; c++) {
-						lo[a][c] = N->lo[a][c];
-						hi[a][c] = N->hi[a][c];
-					}
-#pragma unroll
-				for (int c = 0; c < 4; c++) rf[c] = N->first[c], rc[c] = N->count[c];
-			};
-			fetch(uniform_i32(G->qroot));
-			for (;;) {
-				PROF_BEGIN(tn);
-				ws.add(W_NODES, live);
-				const unsigned long long L = __ballot(live);
-				float tn[4];
-				unsigned long long m[4];
-#pragma unroll
-				for (int c = 0; c < 4; c++) {
-					const float cl[3] = {lo[0][c], lo[1][c], lo[2][c]}, ch[3] = {hi[0][c], hi[1][c], hi[2][c]};
-					const bool h = slab32(cl, ch, r32, lim, tn[c]);
-					m[c] = rc[c] >= 0 ? __ballot(h) & L : 0ull;
-				}
-				// closest hits: near-to-far order of the children for the wave, the entry distances
-				// of its first live lane (children that lane misses last) sorted as integers (the
-				// order of the floats), so that near faces lower the pruning limit early; the
-				// any-hit (shadow) search keeps the stored order.  Any order gives the same results.
-				int ord[4] = {0, 1, 2, 3};
-				if constexpr (!kAnyHit) {
-					const int rep = static_cast<int>(__builtin_ctzll(L));
-					uint32_t key[4];
-#pragma unroll
-					for (int c = 0; c < 4; c++) {
-						const uint32_t u = static_cast<uint32_t>(__builtin_amdgcn_readlane(__float_as_int(tn[c]), rep));
-						const bool mine = (m[c] >> rep) & 1;
-						key[c] = mine ? ((u & 0x80000000u) ? ~u : (u | 0x80000000u)) : 0xfffffff0u + c;
-					}
-					auto cswap = [&](int a, int b) {
-						if (key[ord[b]] < key[ord[a]]) {
-							const int t = ord[a];
-							ord[a] = ord[b];
-							ord[b] = t;
-						}
-					};
-					cswap(0, 1);
-					cswap(2, 3);
-					cswap(0, 2);
-					cswap(1, 3);
-					cswap(1, 2);
-				}
-				PROF_END(ws, PH_NODES, tn);
-				// inner children first, so the node to visit next is known (and its record
-				// requested) before the leaf faces are tested: the nearest inner child next, the
-				// others pushed far to near.  A pushed child keeps this node test's pruning limit
-				// (at most more node visits, never a different result).
-				int32_t next = -1;
-#pragma unroll
-				for (int k = 3; k >= 0; k--) {
-					const int c = ord[k];
-					if (m[c] && rc[c] == 0) {
-						if (next >= 0) wstack[sp++] = next;  // <= kQuadStack (device_types.h)
-						next = rf[c];
-					}
-				}
-				// the leaf children in near order, kept through the next node's fetch
-				int32_t lf[4], lc[4];
-				unsigned long long lm[4];
-				float lt[4];
-#pragma unroll
-				for (int k = 0; k < 4; k++) {
-					const int c = ord[k];
-					lf[k] = rf[c];
-					lc[k] = rc[c];
-					lm[k] = rc[c] > 0 ? m[c] : 0ull;
-					lt[k] = tn[c];
-				}
-				if (next < 0 && sp > 0) next = uniform_i32(wstack[--sp]);
-				if (RT_QUAD_PREFETCH && next >= 0) fetch(next);
-				// each later leaf is tested again against the limit the earlier ones' faces may
-				// have lowered
-				bool tested = false;
-#pragma unroll
-				for (int k = 0; k < 4; k++) {
-					if (!lm[k] || (RT_DIAG_SKIP & 2)) continue;
-					unsigned long long want = lm[k];
-					if (tested) want &= __ballot(live && lt[k] <= lim);
-					if (!want) continue;
-					PROF_BEGIN(tf);
-					const int32_t f0 = fbase + lf[k];
-					for (int32_t f = f0; f < f0 + lc[k]; f++) {
-						const bool hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws,
-						                                          __builtin_amdgcn_inverse_ballot_w64(want) && live);
-						settled = settled || hitf;
-						live = live && !hitf;
-					}
-					lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
-					tested = true;
-					PROF_END(ws, PH_FACES, tf);
-				}
-				if (next < 0 || !wave_any(live)) break;
-				if (!RT_QUAD_PREFETCH) fetch(next);
-			}
 		} else if (!(RT_DIAG_SKIP & 1)) {
 			ws.add(W_ENTRIES, live);
 			const V3 inv = safe_inv(d);

@@ -17,7 +17,6 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DFaceGeo* fgeo;
 	const DFaceNrm* fnrm;
 	const DBvhNode* nodes;
-	const DQuadNode* qnodes;                  // the same trees 4-wide (packet traversal)
 	const int32_t* shadow_order;              // geometry order of the occlusion query
 	// the camera (device copy): read where primary rays are made, not held in registers for
 	// the kernel's lifetime as a 160-B by-value kernel argument would be

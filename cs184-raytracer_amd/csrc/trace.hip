@@ -44,9 +44,8 @@ __device__ __forceinline__ lds_f64* opaque_lds(lds_f64* p) {
 #ifndef RT_FUSED_PARK
 #define RT_FUSED_PARK 1
 #endif
-// entries of a wave-packet traversal's stack (LDS, one per wave): the quad trees need up to
-// three pushes per node
-constexpr int kWaveStack = RT_QUAD ? kQuadStack : kStackDepth;
+// entries of a wave-packet traversal's stack (LDS, one per wave)
+constexpr int kWaveStack = kStackDepth;
 
 // Occupancy targets of the traversal kernels (waves per SIMD, >= 1).  4 (<= 128 VGPRs, a
 // few spills) measured 3 % faster than the compiler's 3 on C3; the wave-packet variants

@@ -174,7 +174,6 @@ def lib() -> ctypes.CDLL:
         "rt_version": (cp, []),
         "rt_device_count": (i32, []),
         "rt_selftest_math": (i32, [i32, i32, vp, vp, vp, i64]),
-        "rt_debug_quad_check": (i32, [vp, ctypes.POINTER(ctypes.c_int64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -390,13 +389,6 @@ class Scene:
         _raise(lib().rt_scene_create_desc(ctypes.byref(d), device, ctypes.byref(p)))
         s._scene = p
         return s
-
-    def quad_check(self) -> tuple:
-        """(violations, quad nodes) of the 4-wide packet trees against the binary LBVHs
-        (rt_debug_quad_check, host only)."""
-        n = ctypes.c_int64(0)
-        bad = lib().rt_debug_quad_check(self._b, ctypes.byref(n))
-        return int(bad), int(n.value)
 
     def digest(self) -> int:
         """Host-side digest of the device scene rt_scene_create would upload (diagnostic)."""

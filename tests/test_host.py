@@ -243,18 +243,3 @@ def test_ctypes_structs_match_the_header_layout(rt, tmp_path):
     assert len(got) == len(want)
     bad = [(w, g) for w, g in zip(want, got) if w[2] != g]
     assert not bad, bad
-
-
-@pytest.mark.parametrize("scene", scene_files())
-def test_quad_trees_reach_the_binary_leaves(rt, scene):
-    """The packet traversal's 4-wide trees (bvh.cpp collapse_quad) group the binary LBVH's
-    nodes without changing what a ray can reach: every leaf exactly once, with the binary
-    tree's padded fp32 box, and a stack bound (kQuadStack) no path exceeds."""
-    s = rt.Scene()
-    try:
-        rt.RTIParser(s).parseFile(os.path.join(SCENES, scene))
-    except rt.RTError:
-        pytest.skip("the scene does not parse")
-    bad, n_quad = s.quad_check()
-    assert bad == 0
-    s.close()
