@@ -149,7 +149,6 @@ struct Lane {
 	// are shaded in batches on shade[3] once the chain has finished
 	hipStream_t shade[4] = {nullptr, nullptr, nullptr, nullptr};
 	int prio_low = 0;
-	std::vector<uint32_t> shade_mask;  // CUs the shading streams may use (RTAMD_SHADE_CUS); empty: all
 	std::vector<LevelBuffers> levels;
 	// RayLevel records of all levels, read by the kernels through the constant address space
 	// (pinned host copy + device copy, updated in stream order when a level is reallocated)
@@ -279,7 +278,6 @@ struct rt_scene {
 	// launch of (hit, light) items: the C4 1/8 row share 0.234 -> 0.208 ms, C1-C4 unchanged
 	// (profiles/round4/ab/latency_quad_fuse_knobs.txt)
 	int64_t fused_min_pixels = 524288;
-	int shade_cus = 0;  // RTAMD_SHADE_CUS: CUs the shading streams may use (0: all; ensure_lanes)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
 	// (no fork/join across queues) and its last kernel finishes the statistics (no
 	// k_stats_finish launch)
@@ -414,11 +412,7 @@ int ensure_events(Lane& ln, size_t level) {
 // (profiles/round4: host traces), and a render of one traced level uses one of the four
 hipStream_t shade_stream(Lane& ln, int k) {
 	if (!ln.shade[k]) {
-		const hipError_t e = ln.shade_mask.empty()
-		                         ? hipStreamCreateWithPriority(&ln.shade[k], hipStreamNonBlocking, ln.prio_low)
-		                         : hipExtStreamCreateWithCUMask(&ln.shade[k], static_cast<uint32_t>(ln.shade_mask.size()),
-		                                                        ln.shade_mask.data());
-		if (e != hipSuccess) {
+		if (hipStreamCreateWithPriority(&ln.shade[k], hipStreamNonBlocking, ln.prio_low) != hipSuccess) {
 			ln.shade[k] = nullptr;
 			return nullptr;
 		}
@@ -1082,17 +1076,6 @@ int ensure_lanes(rt_scene* s, size_t n) {
 			lane_destroy(*ln);
 			return rc;
 		}
-		// RTAMD_SHADE_CUS: the shading streams keep off the remaining CUs, spread evenly over the
-		// chip (CU i kept when the running share floor((i + 1) k / n) steps), so the level chain
-		// always finds free CUs
-		int n_cu = 0;
-		if (s->shade_cus > 0 && hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, s->device) == hipSuccess &&
-		    s->shade_cus < n_cu) {
-			ln->shade_mask.assign((n_cu + 31) / 32, 0u);
-			for (int i = 0; i < n_cu; i++)
-				if (static_cast<int64_t>(i + 1) * s->shade_cus / n_cu > static_cast<int64_t>(i) * s->shade_cus / n_cu)
-					ln->shade_mask[i / 32] |= 1u << (i % 32);
-		}
 		s->lanes.push_back(std::move(ln));
 	}
 	return RT_OK;
@@ -1345,7 +1328,6 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
 	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
-	if (const char* sc = std::getenv("RTAMD_SHADE_CUS")) s->shade_cus = std::max(0, std::atoi(sc));
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
