@@ -278,6 +278,8 @@ struct rt_scene {
 	// launch of (hit, light) items: the C4 1/8 row share 0.234 -> 0.208 ms, C1-C4 unchanged
 	// (profiles/round4/ab/latency_quad_fuse_knobs.txt)
 	int64_t fused_min_pixels = 524288;
+	int merge_joins = 1;    // RTAMD_MERGE_JOINS: the chain waits for the side shading with one event
+	int launch_events = 1;  // RTAMD_LAUNCH_EVENTS: the chain's events recorded by its launches (hipExtLaunchKernel)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
 	// (no fork/join across queues) and its last kernel finishes the statistics (no
 	// k_stats_finish launch)
@@ -641,7 +643,7 @@ struct Render {
 			if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string("planned launch: ") + hipGetErrorString(e));
 		};
 		int launches[3] = {0, 0, 0};
-		std::vector<hipEvent_t> joins;
+		std::vector<std::pair<hipEvent_t, hipStream_t>> joins;  // side shading done, on its stream
 		Plan scratch = pl;
 		// A small chunk (a small frame, or a GPU's row share of one) is issued on ONE stream:
 		// the chain, then every level's shading in one batch, then the reductions.  Waits across
@@ -713,12 +715,17 @@ struct Render {
 				const int remaining = depth - L;
 				const bool last = L == nlev - 1;
 				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
+				// k_closest(L) done: only the side shading of a direct level waits on it; the
+				// launch records it itself (no marker packet in the chain; not under capture)
+				const bool waited = L < direct_levels && !last;
+				hipEvent_t done = waited ? ev(L, 1) : nullptr;
+				if (waited && !done) step(hipErrorOutOfMemory);
+				const bool by_launch = done && s->launch_events && !capture;
 				step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
 				                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
-				                           last && remaining > 0));
+				                           last && remaining > 0, by_launch ? done : nullptr));
 				launches[0]++;
-				hipEvent_t done = ev(L, 1);
-				step(done ? hipEventRecord(done, st) : hipErrorOutOfMemory);
+				if (done && !by_launch) step(hipEventRecord(done, st));
 				// shading beside the chain only where a later level's tracing can overlap it: a
 				// wait on a not yet signalled event of another queue costs tens of microseconds
 				if (L < direct_levels && rc == RT_OK) {
@@ -733,7 +740,7 @@ struct Render {
 					if (side) {
 						hipEvent_t sh = ev(L, 4);
 						step(sh ? hipEventRecord(sh, q) : hipErrorOutOfMemory);
-						joins.push_back(sh);
+						joins.push_back({sh, q});
 					}
 				}
 			}
@@ -751,8 +758,18 @@ struct Render {
 				}
 			}
 		}
-		for (hipEvent_t j : joins)
-			if (rc == RT_OK) step(hipStreamWaitEvent(st, j, 0));
+		// the chain joins the side shading once: the last side stream waits for the others (off
+		// the chain's path, long after they finished) and records again; each wait in the chain's
+		// queue costs ~5 us (not under capture: one event recorded twice)
+		if (joins.size() > 1 && s->merge_joins && !capture && rc == RT_OK) {
+			const auto last_join = joins.back();
+			for (size_t k = 0; k + 1 < joins.size() && rc == RT_OK; k++)
+				if (joins[k].second != last_join.second) step(hipStreamWaitEvent(last_join.second, joins[k].first, 0));
+			step(hipEventRecord(last_join.first, last_join.second));
+			joins.assign(1, last_join);
+		}
+		for (const auto& j : joins)
+			if (rc == RT_OK) step(hipStreamWaitEvent(st, j.first, 0));
 		for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
 			step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1, ln.levels[l].lv,
 			                                ln.levels[l + 1].lv, st));
@@ -1328,6 +1345,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
 	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
+	if (const char* le = std::getenv("RTAMD_LAUNCH_EVENTS")) s->launch_events = std::atoi(le);
+	if (const char* mj = std::getenv("RTAMD_MERGE_JOINS")) s->merge_joins = std::atoi(mj);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));

@@ -126,7 +126,8 @@ enum : int {
 // DERR_PLAN instead of being written (the plan had no further level for it)
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
                           int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
-                          unsigned long long* stats, hipStream_t stream, int packet_mask, int plan_last = 0);
+                          unsigned long long* stats, hipStream_t stream, int packet_mask, int plan_last = 0,
+                          hipEvent_t done = nullptr);
 // Shading of one or more levels in one launch (the deep levels are shaded together once
 // the closest-hit chain has finished).  Items of each level start on a wave boundary so
 // that every wave belongs to one level.  levels_dev: device copy of the RayLevel records.

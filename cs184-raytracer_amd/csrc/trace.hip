@@ -14,6 +14,7 @@
 // Device arithmetic: see intersect.h; pow is glibc's (glibc_pow.h).
 #include <algorithm>
 #include <type_traits>
+#include <hip/hip_ext.h>
 #include "trace.h"
 #include "glibc_pow.h"
 #include "intersect.h"
@@ -1115,17 +1116,24 @@ constexpr int64_t kStrideBlocks = 256 * 8;
 
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
                           int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
-                          unsigned long long* stats, hipStream_t stream, int packet_mask, int plan_last) {
-	if (n <= 0) return hipSuccess;
+                          unsigned long long* stats, hipStream_t stream, int packet_mask, int plan_last,
+                          hipEvent_t done) {
+	if (n <= 0) return done ? hipEventRecord(done, stream) : hipSuccess;
 	const bool packet = packet_mask & (level == 0 ? kPacketClosest0 : level == 1 ? kPacketClosestN | kPacketClosest1 : kPacketClosestN);
 	const int64_t threads = (level == 0 && packet) ? tile_threads(n, fg.width) : n;
 	// with a device-side count, n is an upper bound: a grid of at most kStrideBlocks
 	const unsigned grid = n_dev ? (unsigned)std::min<int64_t>(grid_for(threads, kBlock), kStrideBlocks)
 	                            : grid_for(threads, kBlock);
 	// the counting kernels only for renders that asked for the work counts (work_stats)
+	// done: recorded by the launch itself (the kernel's own completion signal), not by a marker
+	// packet queued behind it: a marker between two kernels of a queue costs ~7 us
 	auto go = [&](auto kernel) {
-		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
-		                   plan_last, levels_dev, ctr, stats);
+		if (done)
+			hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, nullptr, done, 0, s, fg, level, n, n_dev,
+			                      remaining_depth, plan_last, levels_dev, ctr, stats);
+		else
+			hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
+			                   plan_last, levels_dev, ctr, stats);
 	};
 	// instantiations: packet or per lane, counting or not, with or without the mesh search
 	if (s.n_meshes == 0) {
