@@ -1380,7 +1380,14 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	}
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_may_raise = fs.n_may_raise;
-	for (const auto& g : fs.geoms) s->ds.n_meshes += g.kind == rtamd::DGEOM_MESH ? 1 : 0;
+	bool any_bvh = false;
+	for (const auto& g : fs.geoms) {
+		s->ds.n_meshes += g.kind == rtamd::DGEOM_MESH ? 1 : 0;
+		any_bvh = any_bvh || (g.kind == rtamd::DGEOM_MESH && g.bvh_root >= 0);
+	}
+	s->ds.mesh_kind = s->ds.n_meshes == 0 ? 0 : any_bvh ? 2 : 1;
+	// RTAMD_MESH_KIND: a more general instantiation than the scene needs (tests, A/B)
+	if (const char* mk = std::getenv("RTAMD_MESH_KIND")) s->ds.mesh_kind = std::max(s->ds.mesh_kind, std::min(2, std::atoi(mk)));
 	if (const char* ws = std::getenv("RTAMD_WORK_STATS")) s->force_work_stats = std::atoi(ws) != 0;
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	// j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)

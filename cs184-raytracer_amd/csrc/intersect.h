@@ -30,6 +30,12 @@
 namespace rtamd {
 namespace dev {
 
+// What the traversal kernels are instantiated for (template parameter kMesh, chosen on the
+// host from the scene's content): spheres only, meshes all scanned face by face (no LBVH:
+// a mesh of fewer faces than bvh.cpp's threshold, e.g. refraction3's floor triangle), or
+// meshes with LBVHs.  Without the LBVH searches the kernels hold fewer registers.
+constexpr int kMeshNone = 0, kMeshLinear = 1, kMeshBvh = 2;
+
 #ifndef RT_BLOCK
 #define RT_BLOCK 128
 #endif
@@ -490,7 +496,7 @@ __device__ __forceinline__ bool world_cull(GP G, V3 o, V3 winv, double lim) {
 //   prune_cap are skipped (faces there cannot decide it either).  Otherwise completes
 //   like the closest-hit search restricted to dist <= prune_cap.
 // The search itself, without the reference's bounding-box gate (see mesh_hit).
-template <bool kAnyHit, typename GP, typename WS>
+template <bool kAnyHit, int kMesh, typename GP, typename WS>
 __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
                          double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
                          DeviceCounters* ctr, WS& ws) {
@@ -501,7 +507,7 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 	best.dist = INFINITY;
 	best.face = -1;
 	best.id = 0x7fffffff;
-	if (G->bvh_root < 0) {
+	if (kMesh < kMeshBvh || G->bvh_root < 0) {
 		PROF_BEGIN(tf);
 		for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++)
 			if (test_face<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws)) {
@@ -599,11 +605,11 @@ __device__ bool mesh_search(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse
 // The reference tests a gated mesh only when hitsBoundingBox passes (geometry.cpp:72); the
 // search has no side effects, so the gate (six divisions) is evaluated only for rays the
 // search reports a hit (or occluder) for: the same outcome for fewer rays.
-template <bool kAnyHit, typename GP, typename WS>
+template <bool kAnyHit, int kMesh, typename GP, typename WS>
 __device__ bool mesh_hit(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double any_limit,
 double prune_cap, FaceHit& fh, bool& settled, double& found_dist, int32_t* stack,
 DeviceCounters* ctr, WS& ws) {
-if (!mesh_search<kAnyHit>(S, G, o, d, reverse, any_limit, prune_cap, fh, settled, found_dist, stack, ctr, ws))
+if (!mesh_search<kAnyHit, kMesh>(S, G, o, d, reverse, any_limit, prune_cap, fh, settled, found_dist, stack, ctr, ws))
 return false;
 PROF_BEGIN(tg);
 const bool gate_miss = G->gate && !hits_bounding_box(o, d, G->bb_min, G->bb_max);
@@ -633,7 +639,7 @@ __device__ __forceinline__ V3 face_point(const DeviceScene& S, const FaceHit& h)
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	return mk(p0.x + (h.a * va.x + h.b * vb.x), p0.y + (h.a * va.y + h.b * vb.y), p0.z + (h.a * va.z + h.b * vb.z));
 }
-template <bool kMesh>
+template <int kMesh>
 __device__ __forceinline__ V3 hit_point(const DeviceScene& S, const FaceHit& h, V3 oo, V3 dd) {
 	return (!kMesh || h.face < 0) ? oo + h.a * dd : face_point(S, h);
 }
@@ -641,7 +647,7 @@ __device__ __forceinline__ V3 hit_point(const DeviceScene& S, const FaceHit& h, 
 // The closest-hit searches keep only (geometry, face, a, b) of the best hit so far; its
 // world point and object-space normal are recomputed once at the end with the same
 // expressions (bit-identical, fewer live registers during the traversals).
-template <bool kMesh>
+template <int kMesh>
 __device__ __forceinline__ void winner_point_normal(const DeviceScene& S, int g, const FaceHit& h, V3 o, V3 d,
                                                     V3& Pw, V3& No) {
 	const DGeom* G = S.geoms + g;
@@ -676,7 +682,7 @@ __device__ __forceinline__ void check_may_raise(const DeviceScene& S, V3 d, bool
 // object-space transform.
 // kMesh false: a scene of spheres only (DeviceScene::n_meshes == 0), instantiated without
 // the mesh search (fewer registers for the sphere loop: DESIGN.md §4)
-template <bool kMesh, typename WS>
+template <int kMesh, typename WS>
 __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, double& best_dist, int& best_geom, V3& hitP,
                             V3& hitNobj, int32_t* stack, DeviceCounters* ctr, WS& ws) {
 	bool found = false;
@@ -706,7 +712,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 			if (!hit) continue;
 			Pw = xf_point(G->fwd, oo + h.a * dd);
 		} else {
-			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
+			hit = mesh_hit<false, kMesh>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 			if (!hit) continue;
 			Pw = xf_point(G->fwd, face_point(S, h));  // a mesh hit is a face (geometry.cpp:121)
 		}
@@ -728,7 +734,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 // face up to slightly beyond it means no occlusion.  Only a closest face within a
 // relative 1e-7 of the light distance falls back to the reference's full comparison.
 // geom_occludes: geometry G (its world box already passed) occludes the shadow ray.
-template <bool kMesh, typename GP, typename WS>
+template <int kMesh, typename GP, typename WS>
 __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, double dist_light,
                               int32_t* stack, DeviceCounters* ctr, WS& ws) {
 	const bool inf_light = dist_light == INFINITY;
@@ -748,18 +754,18 @@ __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool rever
 		hit = sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
 	} else if (inf_light) {
-		hit = mesh_hit<true>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
+		hit = mesh_hit<true, kMesh>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 	} else {
 		// world distance of object-space dist t is ~ t / nrm
 		const double tl = dist_light * nrm;
 		const double cap = tl * (1.0 + 1e-7) + 1e-300;
-		hit = mesh_hit<true>(S, G, oo, dd, reverse, tl * (1.0 - 1e-7), cap, h, settled, fd, stack, ctr, ws);
+		hit = mesh_hit<true, kMesh>(S, G, oo, dd, reverse, tl * (1.0 - 1e-7), cap, h, settled, fd, stack, ctr, ws);
 		// No face up to `cap` was missed by the capped search, so a closest face beyond
 		// it lies beyond the light.  A closest face inside the 1e-7 band is decided
 		// exactly from the reference's own face choice (full closest-face search).
 		if (hit && !settled) {
 			if (fd > cap) return false;
-			hit = mesh_hit<false>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
+			hit = mesh_hit<false, kMesh>(S, G, oo, dd, reverse, INFINITY, INFINITY, h, settled, fd, stack, ctr, ws);
 		}
 	}
 	if (!hit) return false;
@@ -773,7 +779,7 @@ __device__ __forceinline__ double shadow_slab_limit(double dist_light) {
 }
 
 // The `any` over the geometries, cheap ones first (DeviceScene::shadow_order).
-template <bool kMesh, typename WS>
+template <int kMesh, typename WS>
 __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, int32_t* stack,
                          DeviceCounters* ctr, WS& ws) {
 	const V3 winv = safe_inv(d);
@@ -805,7 +811,7 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 // that index are fetched with scalar loads instead of 64 identical vector loads.
 __device__ __forceinline__ int32_t uniform_i32(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-template <bool kAnyHit, typename GP, typename WS>
+template <bool kAnyHit, int kMesh, typename GP, typename WS>
 __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, bool on, double any_limit,
                                 double prune_cap, FaceHit& fh, bool& settled, double& found_dist,
                                 int32_t* wstack, WS& ws) {
@@ -818,7 +824,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	best.id = 0x7fffffff;
 	bool live = on;
 	if (wave_any(live)) {
-		if (G->bvh_root < 0) {
+		if (kMesh < kMeshBvh || G->bvh_root < 0) {
 			PROF_BEGIN(tf);
 			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++) {
 				const bool hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws, live);
@@ -922,7 +928,7 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	return true;
 }
 
-template <bool kMesh, typename WS>
+template <int kMesh, typename WS>
 __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, bool on, double& best_dist,
                                    int& best_geom, V3& hitP, V3& hitNobj, int32_t* wstack, DeviceCounters* ctr,
                                    WS& ws) {
@@ -951,7 +957,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
 		} else {
-			hit = mesh_hit_packet<false>(S, G, oo, dd, reverse, cand, INFINITY, INFINITY, h, settled, fd, wstack, ws);
+			hit = mesh_hit_packet<false, kMesh>(S, G, oo, dd, reverse, cand, INFINITY, INFINITY, h, settled, fd, wstack, ws);
 		}
 		if (hit) {
 			const V3 Pw = xf_point(G->fwd, hit_point<kMesh>(S, h, oo, dd));
@@ -969,7 +975,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 }
 
 // Packet form of occluded(): same decisions per lane (see occluded()).
-template <bool kMesh, typename WS>
+template <int kMesh, typename WS>
 __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, bool on,
                                 int32_t* wstack, DeviceCounters* ctr, WS& ws) {
 	const bool inf_light = dist_light == INFINITY;
@@ -1005,7 +1011,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		} else {
 			const double tl = inf_light ? INFINITY : dist_light * nrm;
 			const double cap = inf_light ? INFINITY : tl * (1.0 + 1e-7) + 1e-300;
-			hit = mesh_hit_packet<true>(S, G, oo, dd, reverse, cand, inf_light ? INFINITY : tl * (1.0 - 1e-7), cap, h,
+			hit = mesh_hit_packet<true, kMesh>(S, G, oo, dd, reverse, cand, inf_light ? INFINITY : tl * (1.0 - 1e-7), cap, h,
 			                            settled, fd, wstack, ws);
 			// closest face inside the 1e-7 band around the light: the reference's exact choice
 			const bool band = cand && hit && !settled && !inf_light && fd <= cap;
@@ -1014,7 +1020,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 				bool s2;
 				double fd2;
 				FaceHit h2{-1, 0, 0};
-				const bool hit2 = mesh_hit_packet<false>(S, G, oo, dd, reverse, band, INFINITY, INFINITY, h2, s2, fd2,
+				const bool hit2 = mesh_hit_packet<false, kMesh>(S, G, oo, dd, reverse, band, INFINITY, INFINITY, h2, s2, fd2,
 				                                         wstack, ws);
 				if (band) {
 					hit = hit2;

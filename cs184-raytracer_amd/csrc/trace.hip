@@ -67,6 +67,11 @@ constexpr int kWaveStack = kStackDepth;
 #ifndef RT_SPHERE_WAVES
 #define RT_SPHERE_WAVES 5
 #endif
+// Meshes scanned face by face only (kMeshLinear): no LBVH search either, but the fp64 face
+// test's registers (at 5 waves the per-lane kernels spill 18-21 VGPRs)
+#ifndef RT_LINEAR_WAVES
+#define RT_LINEAR_WAVES 4
+#endif
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
 __device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, int W, int H, V3& o, V3& d,
@@ -240,7 +245,7 @@ __device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, 
 	}
 }
 
-template <bool kPacket, bool kMesh, typename NV, typename DV, typename WS>
+template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
 __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, NV n_of, DV dir_of,
                                                bool inside, int32_t* stack, DeviceCounters* ctr,
                                                unsigned long long* stats, WS& ws, double col[3]);
@@ -253,7 +258,7 @@ __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, in
 // kFused (k_fused): the hit is shaded right here, its shadow rays and Phong terms from the
 // hit held in registers (no hit record, no k_shadow / k_shade launch), and the colour goes
 // where fo says.  Never for --intersection-only.
-template <bool kPacket, bool kCount, bool kMesh, bool kFused = false>
+template <bool kPacket, bool kCount, int kMesh, bool kFused = false>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
                                              int remaining, int plan_last, const RayLevel* levels,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
@@ -442,9 +447,9 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 // before the host knows their size: the ray count is read from the previous level's
 // child counter (n_dev) and a fixed grid strides over it, so each level is queued behind
 // the previous one without a host round trip.
-template <bool kPacket, bool kCount, bool kMesh>
+template <bool kPacket, bool kCount, int kMesh>
 __global__ void __launch_bounds__(kBlock)
-    __attribute__((amdgpu_waves_per_eu(!kMesh ? RT_SPHERE_WAVES : kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
+    __attribute__((amdgpu_waves_per_eu(kMesh == kMeshNone ? RT_SPHERE_WAVES : kMesh == kMeshLinear ? RT_LINEAR_WAVES : kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
                                                                       int64_t n_host, const int32_t* n_dev,
                                                                       int remaining, int plan_last,
                                                                       const RayLevel* levels, DeviceCounters* ctr,
@@ -452,8 +457,8 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ AppendLds append_lds;
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
 	// the traversal stacks (LBVH searches: none in a scene of spheres only)
-	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
-	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
+	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
+	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	// level records read through the constant address space (scalar loads at their uses)
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -549,15 +554,15 @@ __device__ void last_block_finish(unsigned long long* stats, DeviceCounters* ctr
 #ifndef RT_FUSED_WAVES
 #define RT_FUSED_WAVES 4
 #endif
-template <bool kPacket, bool kMesh>
+template <bool kPacket, int kMesh>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(RT_FUSED_WAVES))) k_fused(
         DeviceScene S, FrameGeometry fg, int level, int64_t n_host, const int32_t* n_dev, int remaining, int plan_last,
         const RayLevel* levels, DeviceCounters* ctr, unsigned long long* stats, FusedOut fo) {
 	__shared__ AppendLds append_lds;
-	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
+	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ double park_mem[RT_FUSED_PARK && kPacket ? 6 * kBlock : 1];
-	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
+	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
 	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur0.capacity) : n_host;
@@ -681,7 +686,7 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 // colour is the same bits whether the light is occluded or not (it is never -0), so that ray
 // is not traced.  dv_of(): the viewing direction, read only for that test.  Every lane of
 // the wave calls it (kPacket: the search is wave-uniform; lanes without a hit pass on false).
-template <bool kPacket, bool kMesh, typename NV, typename DV, typename WS>
+template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
 __device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P, NV n_of, bool inside, bool zero_mat,
                                               bool on, DV dv_of, int32_t* stack, DeviceCounters* ctr,
                                               unsigned long long* stats, WS& ws) {
@@ -724,7 +729,7 @@ __device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P,
 // A fused level's shading (closest_item<.., kFused>): the verdicts of every light for the
 // hit held in registers, then its Phong terms (scene.cpp:78-108) into col.  on: the lane has
 // a hit to shade (every lane of the wave calls it).
-template <bool kPacket, bool kMesh, typename NV, typename DV, typename WS>
+template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
 __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, NV n_of, DV dir_of,
                                                bool inside, int32_t* stack, DeviceCounters* ctr,
                                                unsigned long long* stats, WS& ws, double col[3]) {
@@ -746,7 +751,7 @@ __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, in
 //    towards each light in turn (one light at a time, still wave-uniform), loading the hit
 //    records once for all lights.
 // The light record of the wave is read with scalar loads.
-template <bool kPacket, bool kCount, bool kMesh>
+template <bool kPacket, bool kCount, int kMesh>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
                                             uint32_t* stat_lds) {
@@ -812,14 +817,14 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 
 // Host-counted batches launch one thread per item; device-counted ones a fixed grid that
 // strides over the items (the bound is block-uniform: no lane of a wave leaves early).
-template <bool kPacket, bool kCount, bool kMesh>
+template <bool kPacket, bool kCount, int kMesh>
 __global__ void __launch_bounds__(kBlock)
-    __attribute__((amdgpu_waves_per_eu(!kMesh && !kPacket ? RT_SPHERE_WAVES : kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
+    __attribute__((amdgpu_waves_per_eu(kMesh == kMeshNone && !kPacket ? RT_SPHERE_WAVES : kMesh == kMeshLinear && !kPacket ? RT_LINEAR_WAVES : kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
-	__shared__ int32_t stack_mem[!kMesh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
+	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
-	int32_t* stack = !kMesh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
+	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
@@ -1114,6 +1119,17 @@ constexpr int64_t kStrideBlocks = 256 * 8;
 
 }  // namespace
 
+// the traversal kernels' instantiation for the scene's geometry (kMeshNone / kMeshLinear /
+// kMeshBvh, DeviceScene::mesh_kind): f(std::integral_constant<int, kind>)
+template <typename F>
+static void by_mesh_kind(const DeviceScene& s, F f) {
+	switch (s.mesh_kind) {
+		case kMeshNone: f(std::integral_constant<int, kMeshNone>{}); break;
+		case kMeshLinear: f(std::integral_constant<int, kMeshLinear>{}); break;
+		default: f(std::integral_constant<int, kMeshBvh>{}); break;
+	}
+}
+
 hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int level, int64_t n, const int32_t* n_dev,
                           int remaining_depth, const RayLevel* levels_dev, DeviceCounters* ctr,
                           unsigned long long* stats, hipStream_t stream, int packet_mask, int plan_last,
@@ -1135,17 +1151,14 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 			hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
 			                   plan_last, levels_dev, ctr, stats);
 	};
-	// instantiations: packet or per lane, counting or not, with or without the mesh search
-	if (s.n_meshes == 0) {
+	// instantiations: packet or per lane, counting or not, by the scene's geometry (mesh_kind)
+	by_mesh_kind(s, [&](auto m) {
+		constexpr int M = decltype(m)::value;
 		if (packet)
-			s.work_stats ? go(k_closest<true, true, false>) : go(k_closest<true, false, false>);
+			s.work_stats ? go(k_closest<true, true, M>) : go(k_closest<true, false, M>);
 		else
-			s.work_stats ? go(k_closest<false, true, false>) : go(k_closest<false, false, false>);
-	} else if (packet) {
-		s.work_stats ? go(k_closest<true, true, true>) : go(k_closest<true, false, true>);
-	} else {
-		s.work_stats ? go(k_closest<false, true, true>) : go(k_closest<false, false, true>);
-	}
+			s.work_stats ? go(k_closest<false, true, M>) : go(k_closest<false, false, M>);
+	});
 	return hipGetLastError();
 }
 
@@ -1173,16 +1186,13 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 	auto go = [&](auto kernel) {
 		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
 	};
-	if (s.n_meshes == 0) {
+	by_mesh_kind(s, [&](auto m) {
+		constexpr int M = decltype(m)::value;
 		if (shadow_packet(b, packet_mask))
-			s.work_stats ? go(k_shadow<true, true, false>) : go(k_shadow<true, false, false>);
+			s.work_stats ? go(k_shadow<true, true, M>) : go(k_shadow<true, false, M>);
 		else
-			s.work_stats ? go(k_shadow<false, true, false>) : go(k_shadow<false, false, false>);
-	} else if (shadow_packet(b, packet_mask)) {
-		s.work_stats ? go(k_shadow<true, true, true>) : go(k_shadow<true, false, true>);
-	} else {
-		s.work_stats ? go(k_shadow<false, true, true>) : go(k_shadow<false, false, true>);
-	}
+			s.work_stats ? go(k_shadow<false, true, M>) : go(k_shadow<false, false, M>);
+	});
 	return hipGetLastError();
 }
 
@@ -1224,10 +1234,10 @@ hipError_t launch_fused(const DeviceScene& s, const FrameGeometry& fg, int level
 		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, fg, level, n, n_dev, remaining_depth,
 		                   plan_last, levels_dev, ctr, stats, fo);
 	};
-	if (s.n_meshes == 0)
-		packet ? go(k_fused<true, false>) : go(k_fused<false, false>);
-	else
-		packet ? go(k_fused<true, true>) : go(k_fused<false, true>);
+	by_mesh_kind(s, [&](auto m) {
+		constexpr int M = decltype(m)::value;
+		packet ? go(k_fused<true, M>) : go(k_fused<false, M>);
+	});
 	return hipGetLastError();
 }
 
