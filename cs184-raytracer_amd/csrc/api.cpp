@@ -238,7 +238,7 @@ struct rt_scene {
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
-	int fuse_shade = 1;                          // RTAMD_FUSE_SHADE: all-lights k_shadow levels shade in place
+	int fuse_shade = 1;                          // RTAMD_FUSE_SHADE: all-lights k_shadow levels shade in place (2: per-lane ones too, scenes without LBVHs)
 	// RTAMD_GRAPH: launch plans of traced chunk shapes: 0 off (every chunk host-driven), 1
 	// replayed as hipGraphs, 2 issued directly (default: this ROCm's graph replay serialises
 	// the branches and the lanes)
@@ -552,7 +552,7 @@ struct Render {
 		HIP_TRY(hipStreamWaitEvent(q, ln.level_events[last][1], 0));
 		HIP_TRY(hipEventRecord(ev[2], q));
 		// one level traced all-lights-per-lane: k_shadow computes the Phong terms itself
-		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(b, s->packet_mask);
+		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, s->fuse_shade >= 2);
 		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) cnt.stage_launches[1]++;
 		HIP_TRY(hipEventRecord(ev[3], q));
@@ -609,7 +609,7 @@ struct Render {
 		// grid sizes from the traced chunk's hits (at least one block: the kernels stride)
 		b.shadow_begin[b.n] = std::max<int64_t>(so, 64);
 		b.shade_begin[b.n] = std::max<int64_t>(ho, 64);
-		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(b, s->packet_mask);
+		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, s->fuse_shade >= 2);
 		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) pl.launches[1]++;
 		if (!b.fused) {

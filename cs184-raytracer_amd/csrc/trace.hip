@@ -69,6 +69,11 @@ constexpr int kWaveStack = kStackDepth;
 #endif
 // Meshes scanned face by face only (kMeshLinear): no LBVH search either, but the fp64 face
 // test's registers (at 5 waves the per-lane kernels spill 18-21 VGPRs)
+// the per-lane all-lights shadow kernels of scenes whose meshes have no LBVH (kMeshLinear)
+// carry the fused Phong terms too (ShadeBatch::fused, RTAMD_FUSE_SHADE=2)
+#ifndef RT_LANE_FUSE_SHADE
+#define RT_LANE_FUSE_SHADE 1
+#endif
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 4
 #endif
@@ -806,8 +811,11 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	if (on) PROF_END(ws, PH_TOTAL, t_total);
 	flush_stats(ws, stats, 1, kPacket);
 	// fused shading (ShadeBatch::fused: all lights of the hit traced by this lane): the Phong
-	// terms of k_shade from the verdicts in registers
-	if (kPacket && B.fused && on) {
+	// terms of k_shade from the verdicts in registers (per-lane kernels: without LBVH
+	// searches only, whose registers leave room for them: 127 VGPRs without spills; the
+	// sphere-only kernel, built for 5 waves, would spill 18)
+	constexpr bool kLaneFuse = RT_LANE_FUSE_SHADE && kMesh == kMeshLinear;
+	if ((kPacket || kLaneFuse) && B.fused && on) {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		const V3 dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
 		shade_hit(S, cur, h, P, N, dv, [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
@@ -1167,7 +1175,9 @@ static bool shadow_packet(const ShadeBatch& b, int packet_mask) {
 	return packet_mask & (lv == 0 ? kPacketShadow0 : (lv == 1 && b.n == 1) ? kPacketShadowN | kPacketShadow1 : kPacketShadowN);
 }
 
-bool shadow_can_fuse(const ShadeBatch& b, int packet_mask) { return b.all_lights && shadow_packet(b, packet_mask); }
+bool shadow_can_fuse(const DeviceScene& s, const ShadeBatch& b, int packet_mask, bool per_lane) {
+	return b.all_lights && (shadow_packet(b, packet_mask) || (per_lane && RT_LANE_FUSE_SHADE && s.mesh_kind == kMeshLinear));
+}
 
 // grid of a device-counted batch: one thread per item of `bound` (an upper bound of its
 // items, from the levels' capacities); the blocks beyond the device count exit at once
