@@ -238,7 +238,9 @@ struct rt_scene {
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
-	int fuse_shade = 1;                          // RTAMD_FUSE_SHADE: all-lights k_shadow levels shade in place (2: per-lane ones too, scenes without LBVHs)
+	// RTAMD_FUSE_SHADE: all-lights k_shadow levels shade in place; 2: the per-lane ones of
+	// scenes whose meshes have no LBVH too (C5 21.92 -> 20.50 ms)
+	int fuse_shade = 2;
 	// RTAMD_GRAPH: launch plans of traced chunk shapes: 0 off (every chunk host-driven), 1
 	// replayed as hipGraphs, 2 issued directly (default: this ROCm's graph replay serialises
 	// the branches and the lanes)
@@ -1368,9 +1370,12 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 		rt_scene_destroy(s.release());
 		return rc;
 	}
-	// light-major single frames pay off where a shadow ray is a long LBVH search; a scene of
-	// spheres only keeps the batch threshold (C2a, one sphere and 5 lights: 0.183 vs 0.217 ms)
-	if (fs.face_geo.empty()) s->light_major_below_single = s->light_major_below_batch;
+	// light-major single frames pay off where a shadow ray is a long LBVH search; a scene
+	// without LBVHs keeps the batch threshold (C2a, one sphere and 5 lights: 0.183 vs 0.217 ms;
+	// C5, whose per-lane all-lights levels then shade in place: 20.41 vs 20.50 ms)
+	bool lbvh = false;
+	for (const auto& g : fs.geoms) lbvh = lbvh || (g.kind == rtamd::DGEOM_MESH && g.bvh_root >= 0);
+	if (!lbvh) s->light_major_below_single = s->light_major_below_batch;
 	{
 		std::vector<rtamd::DCamera> cam(1, fs.camera);
 		if ((rc = upload(s.get(), cam, &s->ds.cam))) {
