@@ -814,7 +814,7 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	// terms of k_shade from the verdicts in registers (per-lane kernels: without LBVH
 	// searches only, whose registers leave room for them: 127 VGPRs without spills; the
 	// sphere-only kernel, built for 5 waves, would spill 18)
-	constexpr bool kLaneFuse = RT_LANE_FUSE_SHADE && kMesh == kMeshLinear;
+	constexpr bool kLaneFuse = (RT_LANE_FUSE_SHADE && kMesh == kMeshLinear) || (RT_LANE_FUSE_SHADE >= 2 && kMesh == kMeshBvh);
 	if ((kPacket || kLaneFuse) && B.fused && on) {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		const V3 dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
@@ -1176,7 +1176,8 @@ static bool shadow_packet(const ShadeBatch& b, int packet_mask) {
 }
 
 bool shadow_can_fuse(const DeviceScene& s, const ShadeBatch& b, int packet_mask, bool per_lane) {
-	return b.all_lights && (shadow_packet(b, packet_mask) || (per_lane && RT_LANE_FUSE_SHADE && s.mesh_kind == kMeshLinear));
+	const bool lane = (RT_LANE_FUSE_SHADE && s.mesh_kind == kMeshLinear) || (RT_LANE_FUSE_SHADE >= 2 && s.mesh_kind == kMeshBvh);
+	return b.all_lights && (shadow_packet(b, packet_mask) || (per_lane && lane));
 }
 
 // grid of a device-counted batch: one thread per item of `bound` (an upper bound of its
