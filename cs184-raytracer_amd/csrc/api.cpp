@@ -149,6 +149,10 @@ struct Lane {
 	// are shaded in batches on shade[3] once the chain has finished
 	hipStream_t shade[4] = {nullptr, nullptr, nullptr, nullptr};
 	int prio_low = 0;
+	// a scene's first call borrows the scene's stream for everything (chain, read-back,
+	// shading: no stream of its own, each costs 8-15 ms to make); the next call gives the
+	// lane its own (upgrade_lane)
+	bool minimal = false;
 	std::vector<LevelBuffers> levels;
 	// RayLevel records of all levels, read by the kernels through the constant address space
 	// (pinned host copy + device copy, updated in stream order when a level is reallocated)
@@ -280,6 +284,8 @@ struct rt_scene {
 	// launch of (hit, light) items: the C4 1/8 row share 0.234 -> 0.208 ms, C1-C4 unchanged
 	// (profiles/round4/ab/latency_quad_fuse_knobs.txt)
 	int64_t fused_min_pixels = 524288;
+	int64_t calls = 0;            // render calls so far
+	int first_call_minimal = 1;   // RTAMD_FIRST_CALL_MINIMAL: the first call makes no streams (Lane::minimal)
 	int shade_blocks_per_cu = 0;  // RTAMD_SHADE_BLOCKS_PER_CU: the shading beside the chain takes at most this many blocks of a CU (0: any)
 	int merge_joins = 1;    // RTAMD_MERGE_JOINS: the chain waits for the side shading with one event
 	int launch_events = 1;  // RTAMD_LAUNCH_EVENTS: the chain's events recorded by its launches (hipExtLaunchKernel)
@@ -416,6 +422,7 @@ int ensure_events(Lane& ln, size_t level) {
 // shading stream k of a lane, made at its first use: a stream costs 7-11 ms to create
 // (profiles/round4: host traces), and a render of one traced level uses one of the four
 hipStream_t shade_stream(Lane& ln, int k) {
+	if (ln.minimal) return ln.stream;
 	if (!ln.shade[k]) {
 		if (hipStreamCreateWithPriority(&ln.shade[k], hipStreamNonBlocking, ln.prio_low) != hipSuccess) {
 			ln.shade[k] = nullptr;
@@ -450,10 +457,24 @@ void lane_destroy(Lane& ln) {
 	for (auto& ev : ln.level_events)
 		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
 	if (ln.chunk_done) (void)hipEventDestroy(ln.chunk_done);
+	if (ln.minimal) return;  // the streams are the scene's
 	for (hipStream_t q : ln.shade)
 		if (q) (void)hipStreamDestroy(q);
 	if (ln.readback) (void)hipStreamDestroy(ln.readback);
 	if (ln.stream) (void)hipStreamDestroy(ln.stream);
+}
+
+// a minimal lane (the scene's first call) gets streams of its own; its buffers, events and
+// plans stay (nothing of them is bound to a stream)
+int upgrade_lane(Lane& ln, int prio_low, int prio_high) {
+	if (!ln.minimal) return RT_OK;
+	HIP_TRY(hipStreamSynchronize(ln.stream));
+	ln.stream = ln.readback = nullptr;
+	ln.minimal = false;
+	HIP_TRY(hipStreamCreateWithPriority(&ln.stream, hipStreamNonBlocking, prio_high));
+	HIP_TRY(hipStreamCreateWithPriority(&ln.readback, hipStreamNonBlocking, prio_high));
+	ln.prio_low = prio_low;
+	return RT_OK;
 }
 
 // image row of the selected-row ordinal q (rt_render_params: blocks of row_block rows)
@@ -1090,10 +1111,25 @@ int64_t selected_rows(const rt_render_params* p) {
 constexpr int kMaxLanes = 8;
 
 // the scene has at least n lanes (each: streams, events; level buffers grow on use)
-int ensure_lanes(rt_scene* s, size_t n) {
+// minimal: a first lane may borrow the scene's stream (Lane::minimal)
+int ensure_lanes(rt_scene* s, size_t n, bool minimal = false) {
+	for (size_t k = 0; k < std::min(n, s->lanes.size()); k++)
+		if (!minimal && s->lanes[k]->minimal) {
+			const int rc = upgrade_lane(*s->lanes[k], s->prio_low, s->prio_high);
+			if (rc) return rc;
+		}
 	while (s->lanes.size() < n) {
 		std::unique_ptr<Lane> ln(new Lane());
-		const int rc = lane_create(*ln, s->prio_low, s->prio_high);
+		int rc;
+		if (minimal && s->lanes.empty()) {
+			ln->stream = ln->readback = s->stream;
+			ln->minimal = true;
+			rc = hipEventCreateWithFlags(&ln->chunk_done, hipEventDisableTiming) == hipSuccess
+			         ? RT_OK
+			         : fail(RT_ERR_DEVICE, "hipEventCreateWithFlags failed");
+		} else {
+			rc = lane_create(*ln, s->prio_low, s->prio_high);
+		}
 		if (rc) {
 			lane_destroy(*ln);
 			return rc;
@@ -1352,6 +1388,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
 	if (const char* le = std::getenv("RTAMD_LAUNCH_EVENTS")) s->launch_events = std::atoi(le);
 	if (const char* mj = std::getenv("RTAMD_MERGE_JOINS")) s->merge_joins = std::atoi(mj);
+	if (const char* fm = std::getenv("RTAMD_FIRST_CALL_MINIMAL")) s->first_call_minimal = std::atoi(fm);
 	if (const char* sb = std::getenv("RTAMD_SHADE_BLOCKS_PER_CU")) s->shade_blocks_per_cu = std::min(16, std::max(0, std::atoi(sb)));
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
@@ -1628,6 +1665,8 @@ std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size
 int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
                      Progress* progress) {
 	const bool batch = jobs.size() > 1;
+	const bool minimal = !batch && s->calls == 0 && s->first_call_minimal && s->lanes.empty() && s->single_lanes == 0;
+	s->calls++;
 	size_t n_lanes = batch ? std::min<size_t>(jobs.size(), s->batch_lanes) : static_cast<size_t>(s->single_lanes);
 	int chunks_per_lane = s->chunks_per_lane;
 	if (!batch && n_lanes == 0) {
@@ -1651,8 +1690,15 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 				n_lanes = 1;
 		}
 		chunks_per_lane = static_cast<int>(std::max<int64_t>(1, (pieces + 1) / 2));
+		// the scene's first call (a CLI run renders one frame): one lane on the scene's own
+		// stream, shading in the chain's stream order; the streams a lane makes cost more than
+		// the frame (8-15 ms each, C3's GPU time is 1.2 ms: profiles/round4 CLI traces)
+		if (minimal) {
+			n_lanes = 1;
+			chunks_per_lane = static_cast<int>(std::max<int64_t>(1, pieces));
+		}
 	}
-	int rc = ensure_lanes(s, n_lanes);
+	int rc = ensure_lanes(s, n_lanes, minimal);
 	if (rc) return rc;
 	Render R{s};
 	R.direct_levels = batch ? s->direct_levels_batch : s->direct_levels_single;

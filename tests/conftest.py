@@ -14,6 +14,10 @@ os.environ.setdefault("RTAMD_LIGHT_MAJOR_BELOW", "0")
 # default so the multi-stream schedule stays covered; odd fuzz seeds and a knob test run it
 os.environ.setdefault("RTAMD_ONE_STREAM_PIXELS", "0")
 os.environ.setdefault("RTAMD_ONE_STREAM_LEVEL1", "0")  # and of plans of one traced level
+# and a scene's first call on its own streams (api.cpp Lane::minimal borrows the scene's stream
+# and shades in the chain's order): most tests render a scene once; the production-schedule
+# tests, odd fuzz seeds and a knob test run the minimal first call
+os.environ.setdefault("RTAMD_FIRST_CALL_MINIMAL", "0")
 for p in (os.path.join(REPO, "cs184-raytracer_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
