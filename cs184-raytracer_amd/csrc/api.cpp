@@ -286,7 +286,6 @@ struct rt_scene {
 	int64_t fused_min_pixels = 524288;
 	int64_t calls = 0;            // render calls so far
 	int first_call_minimal = 1;   // RTAMD_FIRST_CALL_MINIMAL: the first call makes no streams (Lane::minimal)
-	int shade_blocks_per_cu = 0;  // RTAMD_SHADE_BLOCKS_PER_CU: the shading beside the chain takes at most this many blocks of a CU (0: any)
 	int merge_joins = 1;    // RTAMD_MERGE_JOINS: the chain waits for the side shading with one event
 	int launch_events = 1;  // RTAMD_LAUNCH_EVENTS: the chain's events recorded by its launches (hipExtLaunchKernel)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
@@ -613,7 +612,7 @@ struct Render {
 
 	// shading of the levels `lv` with their hit counts read on the device (plans; the grid
 	// from the plan's traced hits)
-	int launch_shading_dev(Lane& ln, const std::vector<int>& lv, hipStream_t q, Plan& pl, bool side = false) {
+	int launch_shading_dev(Lane& ln, const std::vector<int>& lv, hipStream_t q, Plan& pl) {
 		rtamd::ShadeBatch b{};
 		const int64_t nl = s->ds.n_nonambient;
 		auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
@@ -634,12 +633,10 @@ struct Render {
 		b.shadow_begin[b.n] = std::max<int64_t>(so, 64);
 		b.shade_begin[b.n] = std::max<int64_t>(ho, 64);
 		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, s->fuse_shade >= 2);
-		// beside the chain (a side stream): at most RTAMD_SHADE_BLOCKS_PER_CU blocks per CU
-		const unsigned reserve = side ? static_cast<unsigned>(s->shade_blocks_per_cu) : 0u;
-		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask, reserve));
+		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) pl.launches[1]++;
 		if (!b.fused) {
-			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q, reserve));
+			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
 			pl.launches[2]++;
 		}
 		return RT_OK;
@@ -760,7 +757,7 @@ struct Render {
 					if (!q) step(hipErrorOutOfMemory);
 					if (side) step(hipStreamWaitEvent(q, done, 0));
 					scratch.launches[1] = scratch.launches[2] = 0;
-					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch, side);
+					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch);
 					launches[1] += scratch.launches[1];
 					launches[2] += scratch.launches[2];
 					if (side) {
@@ -1389,7 +1386,6 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* le = std::getenv("RTAMD_LAUNCH_EVENTS")) s->launch_events = std::atoi(le);
 	if (const char* mj = std::getenv("RTAMD_MERGE_JOINS")) s->merge_joins = std::atoi(mj);
 	if (const char* fm = std::getenv("RTAMD_FIRST_CALL_MINIMAL")) s->first_call_minimal = std::atoi(fm);
-	if (const char* sb = std::getenv("RTAMD_SHADE_BLOCKS_PER_CU")) s->shade_blocks_per_cu = std::min(16, std::max(0, std::atoi(sb)));
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));

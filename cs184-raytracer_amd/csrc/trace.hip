@@ -14,8 +14,6 @@
 // Device arithmetic: see intersect.h; pow is glibc's (glibc_pow.h).
 #include <algorithm>
 #include <type_traits>
-#include <vector>
-#include <mutex>
 #include <hip/hip_ext.h>
 #include "trace.h"
 #include "glibc_pow.h"
@@ -1191,37 +1189,13 @@ inline unsigned dev_grid(int64_t bound, int block) {
 	return (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(bound, block), RT_DEV_GRID_CAP));
 }
 
-// Dynamic LDS a block of `kernel` holds without using it so that at most `per_cu` of its blocks
-// fit on a CU (160 KB of LDS each): the level chain's next launch then finds room at once
-// (shading beside the chain).  0: none.
-template <typename K>
-static unsigned lds_cap(K kernel, unsigned per_cu) {
-	if (per_cu == 0) return 0;
-	static std::mutex mu;
-	static std::vector<std::pair<const void*, unsigned>> known;  // static LDS per kernel
-	std::lock_guard<std::mutex> lock(mu);
-	const void* key = reinterpret_cast<const void*>(kernel);
-	unsigned stat = 0;
-	bool found = false;
-	for (const auto& k : known)
-		if (k.first == key) stat = k.second, found = true;
-	if (!found) {
-		hipFuncAttributes a{};
-		if (hipFuncGetAttributes(&a, key) != hipSuccess) return 0;
-		stat = static_cast<unsigned>(a.sharedSizeBytes);
-		known.push_back({key, stat});
-	}
-	const unsigned per_block = (160u * 1024u) / per_cu + 1024u;  // just over a 1/per_cu share
-	return per_block > stat ? std::min(per_block - stat, 64u * 1024u) : 0u;
-}
-
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
-                         unsigned long long* stats, hipStream_t stream, int packet_mask, unsigned per_cu) {
+                         unsigned long long* stats, hipStream_t stream, int packet_mask) {
 	const int64_t items = b.shadow_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0 || s.n_nonambient <= 0) return hipSuccess;
 	const unsigned grid = b.dev_counts ? dev_grid(items, kBlock) : grid_for(items, kBlock);
 	auto go = [&](auto kernel) {
-		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), lds_cap(kernel, per_cu), stream, s, b, levels_dev, ctr, stats);
+		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
 	};
 	by_mesh_kind(s, [&](auto m) {
 		constexpr int M = decltype(m)::value;
@@ -1234,11 +1208,11 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 }
 
 hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
-                        DeviceCounters* ctr, hipStream_t stream, unsigned per_cu) {
+                        DeviceCounters* ctr, hipStream_t stream) {
 	const int64_t items = b.shade_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0) return hipSuccess;
 	const unsigned grid = b.dev_counts ? dev_grid(items, kShadeBlock) : grid_for(items, kShadeBlock);
-	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), lds_cap(k_shade, per_cu), stream, s, fg, b, levels_dev, ctr);
+	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, fg, b, levels_dev, ctr);
 	return hipGetLastError();
 }
 
