@@ -22,7 +22,7 @@ ker = sorted(rows("*kernel_trace.csv"), key=lambda r: int(r["Start_Timestamp"]))
 
 
 def kname(r):
-    m = re.search(r"(k_[a-z0-9_]+(?:<[a-z, ]+>)?)\(", r["Kernel_Name"])
+    m = re.search(r"(k_[a-z0-9_]+(?:<[a-z0-9, ]+>)?)\(", r["Kernel_Name"])
     return m.group(1) if m else r["Kernel_Name"][:24]
 
 
