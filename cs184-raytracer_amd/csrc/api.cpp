@@ -228,6 +228,9 @@ struct rt_scene {
 	double* out_dev = nullptr;                   // staging for rt_render (f64)
 	int64_t out_capacity = 0;
 	uint8_t* out8_dev = nullptr;                 // staging for rt_render_rgb8
+	void* host_stage = nullptr;                  // pinned host staging of the image copy (RTAMD_D2H 2)
+	size_t host_stage_bytes = 0;
+	int d2h_mode = 0;                            // RTAMD_D2H (copy_to_host)
 	int64_t out8_capacity = 0;
 	int fail_after = -1;                         // fault injection (rt_debug_fail_after): launches left
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
@@ -1386,6 +1389,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* le = std::getenv("RTAMD_LAUNCH_EVENTS")) s->launch_events = std::atoi(le);
 	if (const char* mj = std::getenv("RTAMD_MERGE_JOINS")) s->merge_joins = std::atoi(mj);
 	if (const char* fm = std::getenv("RTAMD_FIRST_CALL_MINIMAL")) s->first_call_minimal = std::atoi(fm);
+	if (const char* dm = std::getenv("RTAMD_D2H")) s->d2h_mode = std::atoi(dm);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
 	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
 		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
@@ -1490,6 +1494,7 @@ void rt_scene_destroy(rt_scene* s) {
 	for (void* p : s->allocs) (void)hipFree(p);
 	if (s->out_dev) (void)hipFree(s->out_dev);
 	if (s->out8_dev) (void)hipFree(s->out8_dev);
+	if (s->host_stage) (void)hipHostFree(s->host_stage);
 	if (s->summary_host) (void)hipHostFree(s->summary_host);
 	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1907,6 +1912,33 @@ int ensure_staging(rt_scene* s, int64_t n_pixels, bool f64, bool u8) {
 	return RT_OK;
 }
 
+// The image to the caller's (pageable) host memory.  RTAMD_D2H: 0 hipMemcpy (the runtime
+// stages pageable copies itself); 1 the destination pinned for the copy (hipHostRegister);
+// 2 through pinned staging the scene keeps, then memcpy
+hipError_t copy_to_host(rt_scene* s, void* dst, const void* src, size_t bytes) {
+	if (s->d2h_mode == 1) {
+		if (hipHostRegister(dst, bytes, hipHostRegisterDefault) == hipSuccess) {
+			const hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+			(void)hipHostUnregister(dst);
+			return e;
+		}
+	} else if (s->d2h_mode == 2) {
+		if (s->host_stage_bytes < bytes) {
+			if (s->host_stage) (void)hipHostFree(s->host_stage);
+			s->host_stage = nullptr;
+			s->host_stage_bytes = 0;
+			if (hipHostMalloc(&s->host_stage, bytes, hipHostMallocDefault) != hipSuccess) s->host_stage = nullptr;
+			else s->host_stage_bytes = bytes;
+		}
+		if (s->host_stage) {
+			const hipError_t e = hipMemcpy(s->host_stage, src, bytes, hipMemcpyDeviceToHost);
+			if (e == hipSuccess) std::memcpy(dst, s->host_stage, bytes);
+			return e;
+		}
+	}
+	return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+}
+
 bool whole_image(const rt_render_params* p) { return p->row_begin == 0 && p->row_end == p->height && p->row_step == 1; }
 // (row_step 1 selects every row whatever row_block is)
 
@@ -1987,8 +2019,8 @@ int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint
 	if (rc) return rc;
 	rtamd::MarkerRange cr("rtamd: image to host (PCIe)");
 	const double t_copy = now_s();
-	if (out_rgb) HIP_TRY(hipMemcpy(out_rgb, s->out_dev, n * 3 * sizeof(double), hipMemcpyDeviceToHost));
-	if (out_rgb8) HIP_TRY(hipMemcpy(out_rgb8, s->out8_dev, n * 3, hipMemcpyDeviceToHost));
+	if (out_rgb) HIP_TRY(copy_to_host(s, out_rgb, s->out_dev, n * 3 * sizeof(double)));
+	if (out_rgb8) HIP_TRY(copy_to_host(s, out_rgb8, s->out8_dev, n * 3));
 	if (counters) {
 		counters->copy_ms = (now_s() - t_copy) * 1e3;
 		counters->host_ms = (now_s() - t0) * 1e3;
