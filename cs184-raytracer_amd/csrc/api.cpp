@@ -230,7 +230,10 @@ struct rt_scene {
 	uint8_t* out8_dev = nullptr;                 // staging for rt_render_rgb8
 	void* host_stage = nullptr;                  // pinned host staging of the image copy (RTAMD_D2H 2)
 	size_t host_stage_bytes = 0;
-	int d2h_mode = 0;                            // RTAMD_D2H (copy_to_host)
+	int d2h_mode = 0;                            // RTAMD_D2H (copy_to_host, render_to_host)
+	void* mapped_stage = nullptr;                // mapped pinned host image (RTAMD_D2H 3)
+	void* mapped_stage_dev = nullptr;
+	size_t mapped_stage_bytes = 0;
 	int64_t out8_capacity = 0;
 	int fail_after = -1;                         // fault injection (rt_debug_fail_after): launches left
 	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
@@ -1499,6 +1502,7 @@ void rt_scene_destroy(rt_scene* s) {
 	if (s->out_dev) (void)hipFree(s->out_dev);
 	if (s->out8_dev) (void)hipFree(s->out8_dev);
 	if (s->host_stage) (void)hipHostFree(s->host_stage);
+	if (s->mapped_stage) (void)hipHostFree(s->mapped_stage);
 	if (s->summary_host) (void)hipHostFree(s->summary_host);
 	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
 	if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -1943,6 +1947,18 @@ hipError_t copy_to_host(rt_scene* s, void* dst, const void* src, size_t bytes) {
 	return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
 }
 
+// mapped pinned host staging the kernels write the image into (RTAMD_D2H 3)
+int ensure_mapped_stage(rt_scene* s, size_t bytes) {
+	if (s->mapped_stage_bytes >= bytes) return RT_OK;
+	if (s->mapped_stage) (void)hipHostFree(s->mapped_stage);
+	s->mapped_stage = s->mapped_stage_dev = nullptr;
+	s->mapped_stage_bytes = 0;
+	HIP_TRY(hipHostMalloc(&s->mapped_stage, std::max<size_t>(bytes, 256), hipHostMallocMapped));
+	HIP_TRY(hipHostGetDevicePointer(&s->mapped_stage_dev, s->mapped_stage, 0));
+	s->mapped_stage_bytes = bytes;
+	return RT_OK;
+}
+
 bool whole_image(const rt_render_params* p) { return p->row_begin == 0 && p->row_end == p->height && p->row_step == 1; }
 // (row_step 1 selects every row whatever row_block is)
 
@@ -2018,13 +2034,29 @@ int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint
 	if (progress) progress(0, pr.total, user);
 	double* rgb_dev = (out_rgb || p->intersection_only) ? s->out_dev : nullptr;
 	uint8_t* rgb8_dev = out_rgb8 ? s->out8_dev : nullptr;
+	// RTAMD_D2H 3: the kernels write the image straight into mapped pinned host memory (no
+	// copy engine: its first use in a process costs ~16 ms), then a host memcpy
+	const size_t f64_bytes = out_rgb ? static_cast<size_t>(n) * 3 * sizeof(double) : 0, u8_bytes = out_rgb8 ? static_cast<size_t>(n) * 3 : 0;
+	char* mapped = nullptr;
+	if (s->d2h_mode == 3 && (rc = ensure_mapped_stage(s, f64_bytes + u8_bytes)) == RT_OK && s->mapped_stage) {
+		mapped = static_cast<char*>(s->mapped_stage);
+		char* dev = static_cast<char*>(s->mapped_stage_dev);
+		if (out_rgb) rgb_dev = reinterpret_cast<double*>(dev);
+		if (out_rgb8) rgb8_dev = reinterpret_cast<uint8_t*>(dev + f64_bytes);
+	}
+	if (rc) return rc;
 	const double t0 = now_s();
 	rc = render_batch(s, 1, p, &rgb_dev, &rgb8_dev, nullptr, counters, &pr);
 	if (rc) return rc;
 	rtamd::MarkerRange cr("rtamd: image to host (PCIe)");
 	const double t_copy = now_s();
-	if (out_rgb) HIP_TRY(copy_to_host(s, out_rgb, s->out_dev, n * 3 * sizeof(double)));
-	if (out_rgb8) HIP_TRY(copy_to_host(s, out_rgb8, s->out8_dev, n * 3));
+	if (mapped) {
+		if (out_rgb) std::memcpy(out_rgb, mapped, f64_bytes);
+		if (out_rgb8) std::memcpy(out_rgb8, mapped + f64_bytes, u8_bytes);
+	} else {
+		if (out_rgb) HIP_TRY(copy_to_host(s, out_rgb, s->out_dev, f64_bytes));
+		if (out_rgb8) HIP_TRY(copy_to_host(s, out_rgb8, s->out8_dev, u8_bytes));
+	}
 	if (counters) {
 		counters->copy_ms = (now_s() - t_copy) * 1e3;
 		counters->host_ms = (now_s() - t0) * 1e3;
