@@ -318,6 +318,48 @@ struct rt_scene {
 
 namespace {
 
+// The scene's arrays in one device block, filled in one launch from mapped pinned staging
+// (RTAMD_UPLOAD 1): one allocation, no copy engine (its first use in a process costs ~16 ms
+// and every pageable hipMemcpy ~3 ms; profiles/round4 CLI traces).  add() records where each
+// array goes; commit() allocates, stages, copies and sets the device pointers.
+struct UploadBatch {
+	struct Item {
+		const void* host;
+		size_t bytes;
+		const void** dev;
+		size_t offset;
+	};
+	std::vector<Item> items;
+	size_t total = 0;
+	template <typename T>
+	void add(const std::vector<T>& v, const T** dev) {
+		*dev = nullptr;
+		if (v.empty()) return;
+		items.push_back({v.data(), v.size() * sizeof(T), reinterpret_cast<const void**>(dev), total});
+		total += (v.size() * sizeof(T) + 255) & ~size_t(255);
+	}
+	int commit(rt_scene* s) {
+		if (total == 0) return RT_OK;
+		void* block = nullptr;
+		HIP_TRY(hipMalloc(&block, total));
+		s->allocs.push_back(block);
+		void* stage = nullptr;
+		HIP_TRY(hipHostMalloc(&stage, total, hipHostMallocMapped));
+		void* stage_dev = nullptr;
+		hipError_t e = hipHostGetDevicePointer(&stage_dev, stage, 0);
+		for (const Item& it : items) std::memcpy(static_cast<char*>(stage) + it.offset, it.host, it.bytes);
+		if (e == hipSuccess) e = rtamd::launch_copy16(block, stage_dev, static_cast<int64_t>(total / 16), s->stream);
+		if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+		(void)hipHostFree(stage);
+		if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("scene upload: ") + hipGetErrorString(e));
+		for (const Item& it : items) {
+			*it.dev = static_cast<const char*>(block) + it.offset;
+			s->info.device_bytes += static_cast<int64_t>(it.bytes);
+		}
+		return RT_OK;
+	}
+};
+
 template <typename T>
 int upload(rt_scene* s, const std::vector<T>& host, const T** dev) {
 	*dev = nullptr;
@@ -1410,11 +1452,32 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
 	int rc;
-	if ((rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
-	    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
-	    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) ||
-	    (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) ||
-	    (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order))) {
+	const char* um = std::getenv("RTAMD_UPLOAD");
+	const bool batched = !um || std::atoi(um) != 0;
+	UploadBatch ub;
+	std::vector<rtamd::DCamera> cam(1, fs.camera);
+	std::vector<int32_t> shadow_light;  // j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
+	for (size_t li = 0; li < fs.lights.size(); li++)
+		if (fs.lights[li].kind != rtamd::LIGHT_AMBIENT) shadow_light.push_back(static_cast<int32_t>(li));
+	if (batched) {
+		ub.add(fs.geoms, &s->ds.geoms);
+		ub.add(fs.materials, &s->ds.mats);
+		ub.add(fs.lights, &s->ds.lights);
+		ub.add(fs.face_geo, &s->ds.fgeo);
+		ub.add(fs.face_nrm, &s->ds.fnrm);
+		ub.add(fs.nodes, &s->ds.nodes);
+		ub.add(fs.shadow_order, &s->ds.shadow_order);
+		ub.add(cam, &s->ds.cam);
+		ub.add(shadow_light, &s->ds.shadow_light);
+		rc = ub.commit(s.get());
+	} else {
+		(rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
+		    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
+		    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) || (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) ||
+		    (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order)) || (rc = upload(s.get(), cam, &s->ds.cam)) ||
+		    (rc = upload(s.get(), shadow_light, &s->ds.shadow_light));
+	}
+	if (rc) {
 		rt_scene_destroy(s.release());
 		return rc;
 	}
@@ -1424,13 +1487,6 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	bool lbvh = false;
 	for (const auto& g : fs.geoms) lbvh = lbvh || (g.kind == rtamd::DGEOM_MESH && g.bvh_root >= 0);
 	if (!lbvh) s->light_major_below_single = s->light_major_below_batch;
-	{
-		std::vector<rtamd::DCamera> cam(1, fs.camera);
-		if ((rc = upload(s.get(), cam, &s->ds.cam))) {
-			rt_scene_destroy(s.release());
-			return rc;
-		}
-	}
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
 	s->ds.n_may_raise = fs.n_may_raise;
 	bool any_bvh = false;
@@ -1443,15 +1499,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* mk = std::getenv("RTAMD_MESH_KIND")) s->ds.mesh_kind = std::max(s->ds.mesh_kind, std::min(2, std::atoi(mk)));
 	if (const char* ws = std::getenv("RTAMD_WORK_STATS")) s->force_work_stats = std::atoi(ws) != 0;
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
-	// j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
-	std::vector<int32_t> shadow_light;
-	for (size_t li = 0; li < fs.lights.size(); li++)
-		if (fs.lights[li].kind != rtamd::LIGHT_AMBIENT) shadow_light.push_back(static_cast<int32_t>(li));
 	s->ds.n_nonambient = static_cast<int32_t>(shadow_light.size());
-	if ((rc = upload(s.get(), shadow_light, &s->ds.shadow_light))) {
-		rt_scene_destroy(s.release());
-		return rc;
-	}
 	void* c = nullptr;
 	HIP_TRY(hipMalloc(&c, sizeof(rtamd::DeviceCounters)));
 	s->allocs.push_back(c);

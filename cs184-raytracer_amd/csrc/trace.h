@@ -188,6 +188,8 @@ hipError_t launch_fused(const DeviceScene& s, const FrameGeometry& fg, int level
 hipError_t launch_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary,
                                hipStream_t stream);
 hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uint8_t* out_rgb8, hipStream_t stream);
+// n_words 16-byte words from src (device-readable, e.g. mapped pinned host memory) to dst
+hipError_t launch_copy16(void* dst, const void* src, int64_t n_words, hipStream_t stream);
 // Phase profile (builds with -DRT_PHASE_PROF=1 only, else zeros): per (stage, packet) pair
 // (stage 0 k_closest, 1 k_shadow) 8 sums of per-lane shader-clock cycles (intersect.h
 // PhaseSlot); copied and cleared.

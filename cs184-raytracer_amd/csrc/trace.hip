@@ -1262,6 +1262,21 @@ hipError_t launch_stats_finish(unsigned long long* stats, DeviceCounters* ctr, u
 	return hipGetLastError();
 }
 
+// 16-byte words from (mapped pinned) host memory to the device: the scene's arrays in one
+// launch, without the copy engine (api.cpp upload batch)
+__global__ void k_copy16(uint4* dst, const uint4* src, int64_t n) {
+	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_copy16(void* dst, const void* src, int64_t n_words, hipStream_t stream) {
+	if (n_words <= 0) return hipSuccess;
+	const unsigned grid = static_cast<unsigned>(std::min<int64_t>(grid_for(n_words, 256), 4096));
+	hipLaunchKernelGGL(k_copy16, dim3(grid), dim3(256), 0, stream, static_cast<uint4*>(dst), static_cast<const uint4*>(src),
+	                   n_words);
+	return hipGetLastError();
+}
+
 hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uint8_t* out_rgb8, hipStream_t stream) {
 	if (n_values <= 0) return hipSuccess;
 	const double rcp = 1.0 / max_value;  // Color3d /= scalar: multiply by the reciprocal
