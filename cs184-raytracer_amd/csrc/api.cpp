@@ -805,7 +805,7 @@ struct Render {
 				if (L < direct_levels && rc == RT_OK) {
 					const bool side = L < nlev - 1;
 					hipStream_t q = side ? shade_stream(ln, L % 3) : st;
-					if (!q) step(hipErrorOutOfMemory);
+					if (!q && !ln.minimal) step(hipErrorOutOfMemory);
 					if (side) step(hipStreamWaitEvent(q, done, 0));
 					scratch.launches[1] = scratch.launches[2] = 0;
 					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch, side);
@@ -1082,7 +1082,7 @@ struct Render {
 		if (nh > 0) {
 			if (L < direct_levels) {  // big level: shade now, concurrent with k_closest(L+1)
 				hipStream_t q = shade_stream(ln, L % 3);
-				if (!q) return fail(RT_ERR_DEVICE, "shading stream creation failed");
+				if (!q && !ln.minimal) return fail(RT_ERR_DEVICE, "shading stream creation failed");
 				if ((rc = launch_shading(ln, {{L, nh}}, q))) return rc;
 			} else {
 				ln.deferred.push_back({L, nh});
@@ -1092,7 +1092,7 @@ struct Render {
 		for (size_t k = 0, e; k < ln.deferred.size(); k = e) {
 			e = std::min(ln.deferred.size(), k + (static_cast<int>(k) < deep_split ? 1 : rtamd::kMaxBatch));
 			hipStream_t q = shade_stream(ln, 3);
-			if (!q) return fail(RT_ERR_DEVICE, "shading stream creation failed");
+			if (!q && !ln.minimal) return fail(RT_ERR_DEVICE, "shading stream creation failed");
 			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, q))) return rc;
 		}
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
@@ -1449,7 +1449,11 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* bb = std::getenv("RTAMD_BATCH_BALANCE")) s->batch_balance = std::atoi(bb);
 	if (const char* ps = std::getenv("RTAMD_PLAN_SHARE")) s->plan_share = std::atoi(ps);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
-	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+	// RTAMD_SCENE_STREAM 0: the scene works on the null stream instead of a stream of its own
+	// (a stream costs 15-50 ms to create in a fresh process; the lanes' streams are
+	// non-blocking, so the null stream does not serialise with them)
+	const char* ss = std::getenv("RTAMD_SCENE_STREAM");
+	if (!ss || std::atoi(ss) != 0) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
 	int rc;
 	const char* um = std::getenv("RTAMD_UPLOAD");
