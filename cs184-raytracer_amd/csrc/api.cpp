@@ -292,7 +292,6 @@ struct rt_scene {
 	int64_t fused_min_pixels = 524288;
 	int64_t calls = 0;            // render calls so far
 	int first_call_minimal = 1;   // RTAMD_FIRST_CALL_MINIMAL: the first call makes no streams (Lane::minimal)
-	int side_grid_blocks = 0;  // RTAMD_SIDE_GRID_BLOCKS: grid cap of the shading beside the chain (0: none)
 	int merge_joins = 1;    // RTAMD_MERGE_JOINS: the chain waits for the side shading with one event
 	int launch_events = 1;  // RTAMD_LAUNCH_EVENTS: the chain's events recorded by its launches (hipExtLaunchKernel)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
@@ -661,7 +660,7 @@ struct Render {
 
 	// shading of the levels `lv` with their hit counts read on the device (plans; the grid
 	// from the plan's traced hits)
-	int launch_shading_dev(Lane& ln, const std::vector<int>& lv, hipStream_t q, Plan& pl, bool side = false) {
+	int launch_shading_dev(Lane& ln, const std::vector<int>& lv, hipStream_t q, Plan& pl) {
 		rtamd::ShadeBatch b{};
 		const int64_t nl = s->ds.n_nonambient;
 		auto wave_up = [](int64_t x) { return (x + 63) & ~int64_t(63); };
@@ -682,12 +681,10 @@ struct Render {
 		b.shadow_begin[b.n] = std::max<int64_t>(so, 64);
 		b.shade_begin[b.n] = std::max<int64_t>(ho, 64);
 		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, s->fuse_shade >= 2);
-		// beside the chain: at most RTAMD_SIDE_GRID_BLOCKS blocks (a striding grid)
-		const unsigned cap = side ? static_cast<unsigned>(s->side_grid_blocks) : 0u;
-		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask, cap));
+		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) pl.launches[1]++;
 		if (!b.fused) {
-			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q, cap));
+			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
 			pl.launches[2]++;
 		}
 		return RT_OK;
@@ -808,7 +805,7 @@ struct Render {
 					if (!q && !ln.minimal) step(hipErrorOutOfMemory);
 					if (side) step(hipStreamWaitEvent(q, done, 0));
 					scratch.launches[1] = scratch.launches[2] = 0;
-					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch, side);
+					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch);
 					launches[1] += scratch.launches[1];
 					launches[2] += scratch.launches[2];
 					if (side) {
@@ -1436,7 +1433,6 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
 	if (const char* le = std::getenv("RTAMD_LAUNCH_EVENTS")) s->launch_events = std::atoi(le);
 	if (const char* mj = std::getenv("RTAMD_MERGE_JOINS")) s->merge_joins = std::atoi(mj);
-	if (const char* sg = std::getenv("RTAMD_SIDE_GRID_BLOCKS")) s->side_grid_blocks = std::max(0, std::atoi(sg));
 	if (const char* fm = std::getenv("RTAMD_FIRST_CALL_MINIMAL")) s->first_call_minimal = std::atoi(fm);
 	if (const char* dm = std::getenv("RTAMD_D2H")) s->d2h_mode = std::atoi(dm);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);

@@ -150,12 +150,12 @@ struct ShadeBatch {
 
 
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
-                         unsigned long long* stats, hipStream_t stream, int packet_mask, unsigned max_blocks = 0);
+                         unsigned long long* stats, hipStream_t stream, int packet_mask);
 // ShadeBatch::fused may be set only when this holds (the wave-packet all-lights form; with
 // per_lane also the per-lane one of scenes without LBVHs)
 bool shadow_can_fuse(const DeviceScene& s, const ShadeBatch& b, int packet_mask, bool per_lane);
 hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
-                        DeviceCounters* ctr, hipStream_t stream, unsigned max_blocks = 0);
+                        DeviceCounters* ctr, hipStream_t stream);
 // n: the level's ray count, or with n_dev (the previous level's child counter) read on the
 // device (a fixed grid strides over it)
 hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,

@@ -1189,14 +1189,11 @@ inline unsigned dev_grid(int64_t bound, int block) {
 	return (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid_for(bound, block), RT_DEV_GRID_CAP));
 }
 
-// max_blocks: a cap on the grid (the kernels stride over their items), so that a launch beside
-// the level chain leaves no blocks waiting for the CUs the chain's next launch needs (0: none)
 hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
-                         unsigned long long* stats, hipStream_t stream, int packet_mask, unsigned max_blocks) {
+                         unsigned long long* stats, hipStream_t stream, int packet_mask) {
 	const int64_t items = b.shadow_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0 || s.n_nonambient <= 0) return hipSuccess;
-	unsigned grid = b.dev_counts ? dev_grid(items, kBlock) : grid_for(items, kBlock);
-	if (max_blocks) grid = std::min(grid, max_blocks);
+	const unsigned grid = b.dev_counts ? dev_grid(items, kBlock) : grid_for(items, kBlock);
 	auto go = [&](auto kernel) {
 		hipLaunchKernelGGL(kernel, dim3(grid), dim3(kBlock), 0, stream, s, b, levels_dev, ctr, stats);
 	};
@@ -1211,11 +1208,10 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 }
 
 hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
-                        DeviceCounters* ctr, hipStream_t stream, unsigned max_blocks) {
+                        DeviceCounters* ctr, hipStream_t stream) {
 	const int64_t items = b.shade_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0) return hipSuccess;
-	unsigned grid = b.dev_counts ? dev_grid(items, kShadeBlock) : grid_for(items, kShadeBlock);
-	if (max_blocks) grid = std::min(grid, max_blocks);
+	const unsigned grid = b.dev_counts ? dev_grid(items, kShadeBlock) : grid_for(items, kShadeBlock);
 	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, fg, b, levels_dev, ctr);
 	return hipGetLastError();
 }
