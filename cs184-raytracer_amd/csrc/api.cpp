@@ -230,7 +230,9 @@ struct rt_scene {
 	uint8_t* out8_dev = nullptr;                 // staging for rt_render_rgb8
 	void* host_stage = nullptr;                  // pinned host staging of the image copy (RTAMD_D2H 2)
 	size_t host_stage_bytes = 0;
-	int d2h_mode = 0;                            // RTAMD_D2H (copy_to_host, render_to_host)
+	// RTAMD_D2H (copy_to_host, render_to_host): 3, the kernels write the host image into mapped
+	// pinned memory: the CLI's image copy 13-17 ms -> 0.2-2.2 ms (profiles/round4/ab/cli_startup_ab.txt)
+	int d2h_mode = 3;
 	void* mapped_stage = nullptr;                // mapped pinned host image (RTAMD_D2H 3)
 	void* mapped_stage_dev = nullptr;
 	size_t mapped_stage_bytes = 0;
@@ -1445,11 +1447,11 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* bb = std::getenv("RTAMD_BATCH_BALANCE")) s->batch_balance = std::atoi(bb);
 	if (const char* ps = std::getenv("RTAMD_PLAN_SHARE")) s->plan_share = std::atoi(ps);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
-	// RTAMD_SCENE_STREAM 0: the scene works on the null stream instead of a stream of its own
-	// (a stream costs 15-50 ms to create in a fresh process; the lanes' streams are
-	// non-blocking, so the null stream does not serialise with them)
+	// The scene works on the null stream (RTAMD_SCENE_STREAM 1: a stream of its own): a stream
+	// costs 15-50 ms to create in a fresh process (CLI set-up 60 -> 45 ms); the lanes' streams
+	// are non-blocking, so the null stream does not serialise with them
 	const char* ss = std::getenv("RTAMD_SCENE_STREAM");
-	if (!ss || std::atoi(ss) != 0) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+	if (ss && std::atoi(ss) != 0) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
 	int rc;
 	const char* um = std::getenv("RTAMD_UPLOAD");
