@@ -804,7 +804,7 @@ struct Render {
 				if (L < direct_levels && rc == RT_OK) {
 					const bool side = L < nlev - 1;
 					hipStream_t q = side ? shade_stream(ln, L % 3) : st;
-					if (!q && !ln.minimal) step(hipErrorOutOfMemory);
+					if (side && !q && !ln.minimal) step(hipErrorOutOfMemory);  // (the chain's own st may be the null stream)
 					if (side) step(hipStreamWaitEvent(q, done, 0));
 					scratch.launches[1] = scratch.launches[2] = 0;
 					if (rc == RT_OK) rc = launch_shading_dev(ln, {L}, q, scratch);
