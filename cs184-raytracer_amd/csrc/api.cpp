@@ -233,6 +233,7 @@ struct rt_scene {
 	// RTAMD_D2H (copy_to_host, render_to_host): 3, the kernels write the host image into mapped
 	// pinned memory: the CLI's image copy 13-17 ms -> 0.2-2.2 ms (profiles/round4/ab/cli_startup_ab.txt)
 	int d2h_mode = 3;
+	int scene_stream = 1;                        // a stream of its own from the second call on (render_batch)
 	void* mapped_stage = nullptr;                // mapped pinned host image (RTAMD_D2H 3)
 	void* mapped_stage_dev = nullptr;
 	size_t mapped_stage_bytes = 0;
@@ -1447,11 +1448,13 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* bb = std::getenv("RTAMD_BATCH_BALANCE")) s->batch_balance = std::atoi(bb);
 	if (const char* ps = std::getenv("RTAMD_PLAN_SHARE")) s->plan_share = std::atoi(ps);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
-	// The scene works on the null stream (RTAMD_SCENE_STREAM 1: a stream of its own): a stream
-	// costs 15-50 ms to create in a fresh process (CLI set-up 60 -> 45 ms); the lanes' streams
-	// are non-blocking, so the null stream does not serialise with them
+	// The scene's set-up and first call work on the null stream, later calls on a stream of its
+	// own made at the second call (render_batch): a stream costs 15-50 ms to create in a fresh
+	// process (CLI set-up 60 -> 45 ms).  RTAMD_SCENE_STREAM 1: made here; 2: never (null stream)
 	const char* ss = std::getenv("RTAMD_SCENE_STREAM");
-	if (ss && std::atoi(ss) != 0) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+	s->scene_stream = ss ? std::atoi(ss) : 0;
+	if (s->scene_stream == 1) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+	s->scene_stream = s->scene_stream != 2;
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
 	int rc;
 	const char* um = std::getenv("RTAMD_UPLOAD");
@@ -2021,6 +2024,12 @@ int render_batch(rt_scene* s, int n, const rt_render_params* params, double* con
 		if (rc) return rc;
 	}
 	HIP_TRY(hipSetDevice(s->device));
+	// no caller stream: the scene's.  A scene starts on the null stream (a stream costs 15-50 ms
+	// to make in a fresh process, and a CLI run renders once); from its second call on it has
+	// a non-blocking stream of its own: a level chain issued on the null stream beside the
+	// side shading costs C3 6% (1.285 vs 1.214 ms, profiles/round4/ab/latency_scene_stream.txt)
+	if (!stream_v && !s->stream && s->calls > 0 && s->scene_stream)
+		HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
 	// the traversal kernels' instantiation: with the work counters only when asked for
 	s->ds.work_stats = s->force_work_stats;
