@@ -1448,11 +1448,12 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* bb = std::getenv("RTAMD_BATCH_BALANCE")) s->batch_balance = std::atoi(bb);
 	if (const char* ps = std::getenv("RTAMD_PLAN_SHARE")) s->plan_share = std::atoi(ps);
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
-	// The scene's set-up and first call work on the null stream, later calls on a stream of its
-	// own made at the second call (render_batch): a stream costs 15-50 ms to create in a fresh
-	// process (CLI set-up 60 -> 45 ms).  RTAMD_SCENE_STREAM 1: made here; 2: never (null stream)
+	// The scene's own non-blocking stream (work issued without a caller stream).  RTAMD_SCENE_STREAM
+	// 0: the set-up and first call on the null stream and the stream made at the second call
+	// (CLI set-up 32 -> 24 ms), but C3's later single frames then take 1.281 instead of 1.214 ms
+	// (profiles/round4/ab/latency_scene_stream*.txt); 2: always the null stream
 	const char* ss = std::getenv("RTAMD_SCENE_STREAM");
-	s->scene_stream = ss ? std::atoi(ss) : 0;
+	s->scene_stream = ss ? std::atoi(ss) : 1;
 	if (s->scene_stream == 1) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	s->scene_stream = s->scene_stream != 2;
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
@@ -2024,10 +2025,7 @@ int render_batch(rt_scene* s, int n, const rt_render_params* params, double* con
 		if (rc) return rc;
 	}
 	HIP_TRY(hipSetDevice(s->device));
-	// no caller stream: the scene's.  A scene starts on the null stream (a stream costs 15-50 ms
-	// to make in a fresh process, and a CLI run renders once); from its second call on it has
-	// a non-blocking stream of its own: a level chain issued on the null stream beside the
-	// side shading costs C3 6% (1.285 vs 1.214 ms, profiles/round4/ab/latency_scene_stream.txt)
+	// no caller stream: the scene's (RTAMD_SCENE_STREAM 0: made at the second call)
 	if (!stream_v && !s->stream && s->calls > 0 && s->scene_stream)
 		HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
