@@ -69,11 +69,6 @@ constexpr int kWaveStack = kStackDepth;
 #endif
 // Meshes scanned face by face only (kMeshLinear): no LBVH search either, but the fp64 face
 // test's registers (at 5 waves the per-lane kernels spill 18-21 VGPRs)
-// the per-lane all-lights shadow kernels of scenes whose meshes have no LBVH (kMeshLinear)
-// carry the fused Phong terms too (ShadeBatch::fused, RTAMD_FUSE_SHADE=2)
-#ifndef RT_LANE_FUSE_SHADE
-#define RT_LANE_FUSE_SHADE 1
-#endif
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 4
 #endif
@@ -814,7 +809,8 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	// terms of k_shade from the verdicts in registers (per-lane kernels: without LBVH
 	// searches only, whose registers leave room for them: 127 VGPRs without spills; the
 	// sphere-only kernel, built for 5 waves, would spill 18)
-	constexpr bool kLaneFuse = (RT_LANE_FUSE_SHADE && kMesh == kMeshLinear) || (RT_LANE_FUSE_SHADE >= 2 && kMesh == kMeshBvh);
+	// (with LBVH searches it would spill 26 VGPRs; measured neutral on the batch and C3)
+	constexpr bool kLaneFuse = kMesh == kMeshLinear;
 	if ((kPacket || kLaneFuse) && B.fused && on) {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		const V3 dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
@@ -1176,8 +1172,7 @@ static bool shadow_packet(const ShadeBatch& b, int packet_mask) {
 }
 
 bool shadow_can_fuse(const DeviceScene& s, const ShadeBatch& b, int packet_mask, bool per_lane) {
-	const bool lane = (RT_LANE_FUSE_SHADE && s.mesh_kind == kMeshLinear) || (RT_LANE_FUSE_SHADE >= 2 && s.mesh_kind == kMeshBvh);
-	return b.all_lights && (shadow_packet(b, packet_mask) || (per_lane && lane));
+	return b.all_lights && (shadow_packet(b, packet_mask) || (per_lane && s.mesh_kind == kMeshLinear));
 }
 
 // grid of a device-counted batch: one thread per item of `bound` (an upper bound of its
