@@ -247,9 +247,11 @@ struct rt_scene {
 	int direct_levels_single = 3;
 	int direct_levels_batch = 1;
 	int single_lanes = 0;                        // lanes one frame is split over (RTAMD_LANES); 0 = auto
-	// chunk pipelines of a batch in flight (RTAMD_BATCH_LANES): 4 vs 3, C3 bench +0.2-1.2% over
-	// four alternating pairs on two boxes; 8 and smaller chunks lose (profiles/round4/ab/batch_*)
-	int batch_lanes = 4;
+	// chunk pipelines of a batch in flight (RTAMD_BATCH_LANES).  4 lanes gave the C3 bench
+	// +0.2-1.2%, but single frames rendered after such a batch took 1.31-1.34 instead of
+	// 1.16-1.18 ms (its 24 streams share the process's hardware queues differently); 8 lanes and
+	// smaller chunks lose (profiles/round4/ab/batch_*)
+	int batch_lanes = 3;
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
