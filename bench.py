@@ -83,7 +83,7 @@ def parse():
                          "time base")
     ap.add_argument("--solo-only", action="store_true",
                     help="run only the solo pass (the command rocprofv3 profiles for the roofline)")
-    ap.add_argument("--latency-frames", type=int, default=5,
+    ap.add_argument("--latency-frames", type=int, default=11,
                     help="single-frame renders timed after the run (wall-clock latency of one frame)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
