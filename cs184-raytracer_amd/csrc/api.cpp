@@ -2,6 +2,7 @@
 // driver, PNG output.  This is the drop-in for Scene::renderScene (scene.cpp:10-59).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <functional>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -332,7 +333,7 @@ struct UploadBatch {
 	struct Item {
 		const void* host;
 		size_t bytes;
-		const void** dev;
+		std::function<void(const char*)> set;  // stores the array's device address
 		size_t offset;
 	};
 	std::vector<Item> items;
@@ -341,7 +342,7 @@ struct UploadBatch {
 	void add(const std::vector<T>& v, const T** dev) {
 		*dev = nullptr;
 		if (v.empty()) return;
-		items.push_back({v.data(), v.size() * sizeof(T), reinterpret_cast<const void**>(dev), total});
+		items.push_back({v.data(), v.size() * sizeof(T), [dev](const char* p) { *dev = reinterpret_cast<const T*>(p); }, total});
 		total += (v.size() * sizeof(T) + 255) & ~size_t(255);
 	}
 	int commit(rt_scene* s) {
@@ -359,7 +360,7 @@ struct UploadBatch {
 		(void)hipHostFree(stage);
 		if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("scene upload: ") + hipGetErrorString(e));
 		for (const Item& it : items) {
-			*it.dev = static_cast<const char*>(block) + it.offset;
+			it.set(static_cast<const char*>(block) + it.offset);
 			s->info.device_bytes += static_cast<int64_t>(it.bytes);
 		}
 		return RT_OK;
