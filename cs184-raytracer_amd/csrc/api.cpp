@@ -300,7 +300,6 @@ struct rt_scene {
 	int64_t fused_min_pixels = 524288;
 	int64_t calls = 0;            // render calls so far
 	int first_call_minimal = 1;   // RTAMD_FIRST_CALL_MINIMAL: the first call makes no streams (Lane::minimal)
-	int tree_output = 0;    // RTAMD_TREE_OUTPUT: a replayed chunk's reductions per pixel in its output launch
 	int merge_joins = 1;    // RTAMD_MERGE_JOINS: the chain waits for the side shading with one event
 	int launch_events = 1;  // RTAMD_LAUNCH_EVENTS: the chain's events recorded by its launches (hipExtLaunchKernel)
 	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
@@ -744,8 +743,6 @@ struct Render {
 			return on;
 		};
 		const int64_t tiles = ((ln.fg.width + 7) / 8) * ((ln.n0 / ln.fg.width + 7) / 8) * 64;  // level-0 packet threads
-		// the reductions per pixel in the output launch (RTAMD_TREE_OUTPUT): no k_reduce launches
-		const bool tree = s->tree_output && !ln.io && nlev <= 12;
 		if (one_stream(ln, pl) && fusable(ln)) {
 			// every level in one launch (k_fused), level after level; a plan of one level writes
 			// the pixels from there, else the reductions and k_output follow
@@ -762,10 +759,7 @@ struct Render {
 				                         L == nlev - 1 && remaining > 0, fo));
 				launches[0]++;
 			}
-			if (nlev > 1 && tree) {
-				step(rtamd::launch_output_tree(ln.n0, ln.fg, ln.levels_dev, nlev, s->stats, st, s->ctr,
-				                               finish_on(ln.n0, 256) ? &fin : nullptr));
-			} else if (nlev > 1) {
+			if (nlev > 1) {
 				for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
 					step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1,
 					                                ln.levels[l].lv, ln.levels[l + 1].lv, st));
@@ -855,18 +849,12 @@ struct Render {
 		}
 		for (const auto& j : joins)
 			if (rc == RT_OK) step(hipStreamWaitEvent(st, j.first, 0));
-		if (nlev > 1 && tree) {
-			if (rc == RT_OK)
-				step(rtamd::launch_output_tree(ln.n0, ln.fg, ln.levels_dev, nlev, s->stats, st, s->ctr,
-				                               finish_on(ln.n0, 256) ? &fin : nullptr));
-		} else {
-			for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
-				step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1,
-				                                ln.levels[l].lv, ln.levels[l + 1].lv, st));
-			if (rc == RT_OK)
-				step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
-				                          st, s->ctr, finish_on(ln.n0, 256) ? &fin : nullptr));
-		}
+		for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
+			step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1, ln.levels[l].lv,
+			                                ln.levels[l + 1].lv, st));
+		if (rc == RT_OK)
+			step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
+			                          st, s->ctr, finish_on(ln.n0, 256) ? &fin : nullptr));
 		for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
 		for (hipEvent_t e : tmp) (void)hipEventDestroy(e);
 		return rc;
@@ -1453,7 +1441,6 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
 	if (const char* le = std::getenv("RTAMD_LAUNCH_EVENTS")) s->launch_events = std::atoi(le);
 	if (const char* mj = std::getenv("RTAMD_MERGE_JOINS")) s->merge_joins = std::atoi(mj);
-	if (const char* to = std::getenv("RTAMD_TREE_OUTPUT")) s->tree_output = std::atoi(to);
 	if (const char* fm = std::getenv("RTAMD_FIRST_CALL_MINIMAL")) s->first_call_minimal = std::atoi(fm);
 	if (const char* dm = std::getenv("RTAMD_D2H")) s->d2h_mode = std::atoi(dm);
 	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);

@@ -176,11 +176,6 @@ struct FusedOut {
 hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
                          unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr = nullptr,
                          const FusedOut* finish = nullptr);
-// The image with every level's reduction done per pixel (no k_reduce launches): nlev levels of
-// levels_dev, at most 12; not for --intersection-only
-hipError_t launch_output_tree(int64_t n, const FrameGeometry& fg, const RayLevel* levels_dev, int nlev,
-                              unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr,
-                              const FusedOut* finish = nullptr);
 // One level in one launch (k_fused): closest hits, children, and every hit's shadow rays and
 // Phong terms from registers (the level's k_closest + k_shadow + k_shade); never for
 // --intersection-only or counting renders.  Arguments as launch_closest.

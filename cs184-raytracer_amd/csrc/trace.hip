@@ -922,75 +922,6 @@ __global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lv
 	if (fo.summary) last_block_finish(stats, ctr, fo);
 }
 
-// The image with every level's reduction done per pixel (RTAMD_TREE_OUTPUT; replaces the
-// k_reduce launches and k_output): the pixel's ray tree is walked depth first, each ray's
-// colour = (local + refraction child's) + reflection child's * kr, children reduced first
-// (reduce_colour's operations in its order, scene.cpp:127,134), down to level nlev - 1, whose
-// colours are the shaded ones.  nlev <= kTreeLevels.
-constexpr int kTreeLevels = 12;
-__global__ void k_output_tree(int64_t n, FrameGeometry fg, const RayLevel* levels, int nlev,
-                              unsigned long long* stats, DeviceCounters* ctr, FusedOut fo) {
-	const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-	const auto& lv0 = *uniform_ptr(levels);
-	if (i0 == 0) lv0.counts[0] = lv0.counts[1] = 0;  // level 0's counts, for the lane's next chunk
-	if (i0 < n) {
-		int32_t idx[kTreeLevels];
-		uint8_t st[kTreeLevels];  // 0 start, 1 refraction child pending/done, 2 reflection child, 3 leaf level
-		double acc[kTreeLevels][3];
-		int sp = 0;
-		idx[0] = static_cast<int32_t>(i0);
-		st[0] = 0;
-		for (;;) {
-			const RayLevel* L = levels + sp;
-			const int32_t i = idx[sp];
-			if (st[sp] == 0) {
-				acc[sp][0] = L->cr[i];
-				acc[sp][1] = L->cg[i];
-				acc[sp][2] = L->cb[i];
-				if (sp + 1 < nlev) {
-					st[sp] = 1;
-					const int32_t t = L->child_refr[i];
-					if (t >= 0) {
-						idx[++sp] = t;
-						st[sp] = 0;
-						continue;
-					}
-				} else {
-					st[sp] = 3;
-				}
-			}
-			if (st[sp] == 1) {
-				st[sp] = 2;
-				const int32_t r = L->child_refl[i];
-				if (r >= 0) {
-					idx[++sp] = r;
-					st[sp] = 0;
-					continue;
-				}
-				st[sp] = 3;  // no reflection child: done
-			}
-			// acc[sp] is this ray's reduced colour: hand it to the parent
-			if (sp == 0) break;
-			const double c0 = acc[sp][0], c1 = acc[sp][1], c2 = acc[sp][2];
-			sp--;
-			const RayLevel* P = levels + sp;
-			if (st[sp] == 1) {  // the refraction child
-				acc[sp][0] = acc[sp][0] + c0;
-				acc[sp][1] = acc[sp][1] + c1;
-				acc[sp][2] = acc[sp][2] + c2;
-			} else {  // the reflection child (st 2)
-				const int32_t pi = idx[sp];
-				acc[sp][0] = acc[sp][0] + c0 * P->kr[pi];
-				acc[sp][1] = acc[sp][1] + c1 * P->kg[pi];
-				acc[sp][2] = acc[sp][2] + c2 * P->kb[pi];
-				st[sp] = 3;
-			}
-		}
-		write_pixel(fg, i0, acc[0], true);
-	}
-	if (fo.summary) last_block_finish(stats, ctr, fo);
-}
-
 // one block of kStatShards threads: thread t owns shard t; tree reduction in LDS
 __global__ void k_stats_finish(unsigned long long* stats, DeviceCounters* ctr, unsigned long long* summary) {
 	__shared__ unsigned long long red[kStatShards][ST_COUNT + 1];
@@ -1294,15 +1225,6 @@ hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl
 	const FusedOut fo = finish ? *finish : FusedOut{};
 	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, fg, lvl0, lvl1 ? *lvl1 : lvl0,
 	                   lvl1 ? 1 : 0, stats, ctr, fo);
-	return hipGetLastError();
-}
-
-hipError_t launch_output_tree(int64_t n, const FrameGeometry& fg, const RayLevel* levels_dev, int nlev,
-                              unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr, const FusedOut* finish) {
-	if (n <= 0) return hipSuccess;
-	if (nlev < 1 || nlev > kTreeLevels) return hipErrorInvalidValue;
-	const FusedOut fo = finish ? *finish : FusedOut{};
-	hipLaunchKernelGGL(k_output_tree, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, fg, levels_dev, nlev, stats, ctr, fo);
 	return hipGetLastError();
 }
 
