@@ -19,7 +19,11 @@ CLI = os.path.join(REPO, "oracle", "cpu_bvh_cli")
 
 @pytest.fixture(scope="module")
 def cpu_bvh():
-    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "cpu_bvh_cli"], check=True)
+    import fcntl
+    # one make at a time (pytest-xdist workers would otherwise race on the same binary)
+    with open(os.path.join(REPO, "oracle", ".make.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "cpu_bvh_cli"], check=True)
     return CLI
 
 
