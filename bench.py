@@ -47,6 +47,10 @@ HBM_PEAK_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md, memory hie
 # L2, measured 16.8-18.8 TB/s (MI355X_MICROARCH.md "Indexed rows: gather into LDS", the table's
 # first row); the upper figure is the roof (the scene's nodes and faces are such shared rows)
 L2_PEAK_GBS = 18800.0
+# the hardware's aggregate L2 bandwidth (8 XCDs x 4 MiB L2, the round-1..3 roof): reported
+# beside the measured gather ceiling as `l2_aggregate`, so that earlier rounds' L2 fractions
+# (taken against this figure) stay comparable
+L2_AGGREGATE_GBS = 34500.0
 FP64_PEAK_TFLOPS = 78.6     # MI355X vector FP64
 NODE_BYTES, TRI_BYTES, NRM_BYTES = 64, 72, 72   # SURVEY.md §8d algorithmic bytes (64-B fp32-box node)
 RAY_IO_BYTES, PIXEL_BYTES = 64 + 64, 24
@@ -122,12 +126,37 @@ def latest_traffic():
     return old if os.path.exists(old) else None
 
 
-def _cores():
+def core_info():
+    """The host cores the CPU baseline may use, with the evidence: every
+    CPU of this process's affinity set, capped by the cgroup CPU quota when one is set (the
+    container's real share of a machine whose nproc counts every CPU) and by OMP_NUM_THREADS
+    when the environment sets it (the GPU box sets it to its CPU share)."""
+    nproc = os.cpu_count() or 1
     try:
-        n = len(os.sched_getaffinity(0))
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))  # the GPU box's CPU share is 16
+        affinity = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    cores, rule = affinity, "affinity set"
+    if quota is not None and int(quota) < cores:
+        cores, rule = max(1, int(quota)), "cgroup cpu.max quota"
+    if omp is not None and omp < cores:
+        cores, rule = omp, "OMP_NUM_THREADS (the box's CPU share)"
+    return {"nproc": nproc, "affinity": affinity, "cgroup_quota_cpus": quota, "omp_num_threads": omp,
+            "cores": cores, "rule": "cores = min(affinity, cgroup quota, OMP_NUM_THREADS): " + rule}
+
+
+def _cores():
+    return core_info()["cores"]
 
 
 def cpu_model():
@@ -361,6 +390,9 @@ def roofline(solo, frames, traffic_path, concurrent, valu_path=None):
                "what": "SURVEY.md §8d algorithmic bytes (ray I/O + LBVH nodes + triangles + normals; the scene "
                        "is L2/MALL-resident) / solo launch time vs the chip's measured L2-served gather rate "
                        "(18.8 TB/s, MI355X_MICROARCH.md 'Indexed rows: gather into LDS')"},
+        "l2_aggregate": {"achieved": alg_bytes / t_launch_s / 1e9, "peak": L2_AGGREGATE_GBS, "unit": "GB/s",
+                         "what": "the same bytes vs the aggregate L2 bandwidth (34.5 TB/s) that rounds 1-3 used as "
+                                 "the L2 roof (for comparison with them; the gather ceiling above is the roof)"},
         "fp64": {"achieved": flops / t_launch_s / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                  "what": "SURVEY.md §8d algorithmic FP64 flops / solo launch time vs vector FP64 peak"},
     }
@@ -385,7 +417,7 @@ def roofline(solo, frames, traffic_path, concurrent, valu_path=None):
         r["frac"] = r["achieved"] / r["peak"]
         r["achieved"] = round(r["achieved"], 3)
         r["frac"] = round(r["frac"], 4)
-    bound = max(roofs, key=lambda k: roofs[k]["frac"])
+    bound = max((k for k in roofs if k != "l2_aggregate"), key=lambda k: roofs[k]["frac"])
     b = roofs[bound]
     return {
         "bound": bound, "achieved": b["achieved"], "peak": b["peak"], "unit": b["unit"], "frac": b["frac"],
@@ -777,6 +809,8 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(s, scene, W, H, kw["bdepth"], a.cpu_seconds)
             res["cpu_baseline"]["cpu_model"] = cpu_model()
+            ci = core_info()
+            res["cpu_baseline"].update({"nproc": ci["nproc"], "affinity": ci["affinity"], "host_cpus": ci})
             one = reference_single_thread(s, scene, W, H, kw["bdepth"], a.cpu_seconds / 3)
             if one:
                 res["cpu_baseline"]["single_thread"] = one

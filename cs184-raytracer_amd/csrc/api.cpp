@@ -134,7 +134,10 @@ struct Plan {
 	// rays and hits of every level in the traced chunk: they size the grids only (the kernels
 	// read the actual counts and stride over them, so a difference costs time, not results)
 	std::vector<int64_t> level_n, hits;
-	std::vector<int64_t> capacity;  // the building lane's level buffer capacities (plan sharing)
+	// the level buffer capacities a replay needs (plan sharing, right-sizing): the traced
+	// chunk's ray counts, which a replay of the same key reproduces exactly (same rows, same
+	// scene), not the host-driven trace's one-level-lookahead bounds
+	std::vector<int64_t> capacity;
 	int launches[3] = {0, 0, 0};
 	hipGraphExec_t exec = nullptr;
 };
@@ -155,6 +158,10 @@ struct Lane {
 	// lane its own (upgrade_lane)
 	bool minimal = false;
 	std::vector<LevelBuffers> levels;
+	// the largest ray count of each level traced host-driven during the current call, and
+	// whether a level buffer grew in it (right_size_levels)
+	std::vector<int64_t> call_need;
+	bool grew = false;
 	// RayLevel records of all levels, read by the kernels through the constant address space
 	// (pinned host copy + device copy, updated in stream order when a level is reallocated)
 	rtamd::RayLevel* levels_pinned = nullptr;
@@ -298,6 +305,11 @@ struct rt_scene {
 	// launch of (hit, light) items: the C4 1/8 row share 0.234 -> 0.208 ms, C1-C4 unchanged
 	// (profiles/round4/ab/latency_quad_fuse_knobs.txt)
 	int64_t fused_min_pixels = 524288;
+	// RTAMD_LEVEL_BUDGET: bytes of level buffers all lanes may hold together (0: no limit).  A
+	// render whose host-driven trace would need more is redone with chunks of half as many
+	// pixels (budget_chunk_pixels, kept for later calls) until it fits (render_jobs)
+	int64_t level_budget = 0;
+	int64_t budget_chunk_pixels = 0;
 	int64_t calls = 0;            // render calls so far
 	int first_call_minimal = 1;   // RTAMD_FIRST_CALL_MINIMAL: the first call makes no streams (Lane::minimal)
 	int merge_joins = 1;    // RTAMD_MERGE_JOINS: the chain waits for the side shading with one event
@@ -380,13 +392,30 @@ int upload(rt_scene* s, const std::vector<T>& host, const T** dev) {
 	return RT_OK;
 }
 
-// Level buffers grow on demand and are kept for later renders (HBM is plentiful:
-// ~130 B per ray record).
-int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
-	if (ln.levels.size() <= level) ln.levels.resize(level + 1);
+// Level buffers grow on demand during a host-driven trace (one level of lookahead: up to
+// four times the rays a level ends up holding), are cut back to what the lane's launch plans
+// need once the call is done (right_size_levels), and are kept for later renders.
+// bytes of one level buffer of `n` ray slots: 21 double arrays, 4 int32 arrays, two flag
+// arrays, n x lights shadow verdicts and the level's counts, each 256-B aligned
+int64_t level_block_bytes(const rt_scene* s, int64_t n) {
+	const int64_t nl = std::max(1, s->ds.n_nonambient);
+	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+	return 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
+}
+
+constexpr int kBudgetMiss = 2;  // internal return code: RTAMD_LEVEL_BUDGET exceeded (render_jobs)
+
+// (Re)allocates level `level` for `capacity` slots (at least 1024), larger or smaller than
+// it was; kBudgetMiss when the lanes' level buffers would exceed RTAMD_LEVEL_BUDGET
+int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	LevelBuffers& L = ln.levels[level];
-	if (L.lv.capacity >= capacity) return RT_OK;
-	clear_plans(ln);  // the plans' graphs hold this lane's buffer pointers
+	capacity = std::max<int64_t>(capacity, 1024);
+	const int64_t n = capacity;
+	const int64_t nl = std::max(1, s->ds.n_nonambient);
+	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
+	const int64_t bytes = level_block_bytes(s, n);
+	if (s->level_budget > 0 && s->info.level_bytes - L.bytes + bytes > s->level_budget) return kBudgetMiss;
+	if (s->graphs == 1) clear_plans(ln);  // captured graphs hold this lane's buffer pointers
 	if (L.block) {
 		HIP_TRY(hipDeviceSynchronize());
 		HIP_TRY(hipFree(L.block));
@@ -394,16 +423,10 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		s->info.level_bytes -= L.bytes;
 		L.bytes = 0;
 	}
-	capacity = std::max<int64_t>(capacity, 1024);
-	const int64_t n = capacity;
-	const int64_t nl = std::max(1, s->ds.n_nonambient);
-	// 21 double arrays, 4 int32 arrays, two flag arrays, n x lights shadow verdicts and the
-	// level's counts, each 256-B aligned
-	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	const int64_t bytes = 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
 	HIP_TRY(hipMalloc(&L.block, bytes));
 	L.bytes = bytes;
 	s->info.level_bytes += bytes;
+	s->info.level_bytes_peak = std::max(s->info.level_bytes_peak, s->info.level_bytes);
 	char* p = static_cast<char*>(L.block);
 	auto take = [&](int64_t b) {
 		char* r = p;
@@ -425,6 +448,13 @@ int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	HIP_TRY(hipMemset(L.lv.counts, 0, 4 * sizeof(int32_t)));
 	L.lv.capacity = capacity;
 	return RT_OK;
+}
+
+int ensure_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
+	if (ln.levels.size() <= level) ln.levels.resize(level + 1);
+	if (ln.levels[level].lv.capacity >= capacity) return RT_OK;
+	ln.grew = true;
+	return alloc_level(s, ln, level, capacity);
 }
 
 // Level `level` exists and its RayLevel record is in the pinned array (the record of an
@@ -868,7 +898,7 @@ struct Render {
 		pl.n_levels = static_cast<int>(ln.level_n.size());
 		pl.level_n = ln.level_n;
 		for (int L = 0; L < pl.n_levels; L++) pl.hits.push_back(ln.counts_host[2 * L]);
-		for (int L = 0; L < pl.n_levels; L++) pl.capacity.push_back(ln.levels[L].lv.capacity);
+		for (int L = 0; L < pl.n_levels; L++) pl.capacity.push_back(std::max<int64_t>(pl.level_n[L], 1));
 		if (s->plan_truncate && pl.n_levels > 1) pl.n_levels--;  // test hook: a plan that must miss
 		if (s->graphs == 1) {
 			hipGraph_t graph = nullptr;
@@ -910,7 +940,9 @@ struct Render {
 		if (s->graphs != 2 || s->serial || !s->plan_share) return nullptr;
 		for (const Plan& q : s->shared_plans) {
 			if (!(q.key == k)) continue;
-			for (int L = 0; L < q.n_levels && rc == RT_OK; L++) rc = ensure_level_record(s, ln, L, q.capacity[L]);
+			// (and the level past the last: its k_closest clears that level's counts)
+			for (int L = 0; L <= q.n_levels && rc == RT_OK; L++)
+				rc = ensure_level_record(s, ln, L, L < q.n_levels ? q.capacity[L] : 1024);
 			if (rc) return nullptr;
 			keep_plan(ln, q);
 			return &ln.plans.back();
@@ -1126,6 +1158,8 @@ struct Render {
 			if (progress) progress->done += ln.n0;
 			return RT_OK;
 		}
+		if (ln.call_need.size() < ln.level_n.size()) ln.call_need.resize(ln.level_n.size(), 0);
+		for (size_t L = 0; L < ln.level_n.size(); L++) ln.call_need[L] = std::max(ln.call_need[L], ln.level_n[L]);
 		if (s->graphs && !s->serial && !find_plan(ln, key_of(ln))) {
 			const int rc = build_plan(ln);
 			if (rc) return rc;
@@ -1293,6 +1327,7 @@ int scene_from_desc(const rt_scene_desc& d, rtamd::Scene& sc) {
 extern "C" {
 
 const char* rt_last_error(void) { return g_error.c_str(); }
+int rt_abi_version(void) { return RTAMD_ABI_VERSION; }
 const char* rt_version(void) { return "rtamd 0.1 (gfx950)"; }
 
 rt_builder* rt_builder_create(void) { return new rt_builder(); }
@@ -1452,6 +1487,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* bc = std::getenv("RTAMD_BATCH_CHUNK")) s->batch_chunk_pixels = std::max<int64_t>(1, std::atoll(bc));
 	if (const char* bb = std::getenv("RTAMD_BATCH_BALANCE")) s->batch_balance = std::atoi(bb);
 	if (const char* ps = std::getenv("RTAMD_PLAN_SHARE")) s->plan_share = std::atoi(ps);
+	if (const char* lb = std::getenv("RTAMD_LEVEL_BUDGET")) s->level_budget = std::max<int64_t>(0, std::atoll(lb));
+	s->info.level_budget = s->level_budget;
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
 	// The scene's own non-blocking stream (work issued without a caller stream).  RTAMD_SCENE_STREAM
 	// 0: the set-up and first call on the null stream and the stream made at the second call
@@ -1615,9 +1652,89 @@ constexpr int kPlanMiss = 1;  // internal return code of render_jobs_impl (never
 
 int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
                      Progress* progress);
+int render_jobs_once(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
+                     Progress* progress);
+constexpr int64_t kMinBudgetChunkPixels = 1 << 14;
+
+// After a call whose host-driven traces grew level buffers: every lane's levels cut back to
+// what its launch plans replay and this call traced (the exact ray counts of each level:
+// a replay of a plan's chunk reproduces them), so that the one-level-lookahead bounds of the
+// host-driven trace (up to four times a level's rays) are not kept between calls.  C5 held
+// 59 GiB of level buffers after one frame in round 4 (missing 3).
+int right_size_levels(rt_scene* s) {
+	if (s->graphs == 1) return RT_OK;  // captured graphs hold the buffers' addresses
+	for (auto& lp : s->lanes) {
+		Lane& ln = *lp;
+		if (!ln.grew) continue;
+		ln.grew = false;
+		std::vector<int64_t> need = ln.call_need;
+		need.resize(ln.levels.size(), 0);
+		for (const Plan& pl : ln.plans)
+			for (int L = 0; L < pl.n_levels && L < static_cast<int>(need.size()); L++)
+				need[L] = std::max(need[L], pl.capacity[L]);
+		for (size_t L = 0; L < ln.levels.size(); L++) {
+			const int64_t target = std::max<int64_t>(need[L], 1024);
+			const int64_t cap = ln.levels[L].lv.capacity;
+			if (cap <= target + target / 4 + 65536) continue;  // hysteresis: no churn for small differences
+			int rc = alloc_level(s, ln, L, target);
+			if (!rc) rc = ensure_level_record(s, ln, L, 0);  // the device copy of its RayLevel record
+			if (rc) return rc;
+		}
+		ln.call_need.clear();
+	}
+	return RT_OK;
+}
+
+// RTAMD_LEVEL_BUDGET exceeded: the call's work is dropped, every level buffer freed and the
+// chunks halved (kept for later calls); fails when even small chunks do not fit
+int shrink_for_budget(rt_scene* s, int64_t first_chunk_pixels) {
+	reset_after_error(s);
+	for (auto& lp : s->lanes) {
+		Lane& ln = *lp;
+		clear_plans(ln);
+		for (size_t L = 0; L < ln.levels.size(); L++) {
+			int rc = alloc_level(s, ln, L, 1024);
+			if (rc == kBudgetMiss) return fail(RT_ERR_DEVICE, "RTAMD_LEVEL_BUDGET is smaller than the minimal level buffers");
+			if (rc || (rc = ensure_level_record(s, ln, L, 0))) return rc;
+		}
+		ln.call_need.clear();
+		ln.grew = false;
+	}
+	s->shared_plans.clear();
+	const int64_t cur = s->budget_chunk_pixels > 0 ? s->budget_chunk_pixels : first_chunk_pixels;
+	const int64_t next = cur / 2;
+	if (next < kMinBudgetChunkPixels)
+		return fail(RT_ERR_DEVICE, "the level buffers of a " + std::to_string(cur) +
+		                               "-pixel chunk exceed RTAMD_LEVEL_BUDGET (" + std::to_string(s->level_budget) + " bytes)");
+	s->budget_chunk_pixels = next;
+	return RT_OK;
+}
 
 int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
                 Progress* progress = nullptr) {
+	int rc;
+	for (;;) {
+		rc = render_jobs_once(s, jobs, caller, counters, progress);
+		if (rc != kBudgetMiss) break;
+		int64_t first = (int64_t)1 << 22;
+		for (const Job& j : jobs)
+			if (j.p->chunk_pixels > 0) first = std::min<int64_t>(first, j.p->chunk_pixels);
+		if ((rc = shrink_for_budget(s, first))) break;
+		if (progress) progress->done = 0;
+	}
+	if (rc == RT_OK) rc = right_size_levels(s);
+	// a device MathException is reported after a complete render (nothing in flight, the
+	// statistics already cleared by k_stats_finish); any other error may leave work queued
+	if (rc && rc != RT_ERR_MATH) {
+		const std::string err = g_error;
+		reset_after_error(s);
+		g_error = err;
+	}
+	return rc;
+}
+
+int render_jobs_once(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
+                     Progress* progress) {
 	int rc = render_jobs_impl(s, jobs, caller, counters, progress);
 	if (rc == kPlanMiss) {
 		// a replayed plan did not fit (DERR_PLAN: a level it lacked, or a level larger than
@@ -1633,20 +1750,21 @@ int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_coun
 		s->graphs = graphs;
 		if (rc == kPlanMiss) rc = fail(RT_ERR_DEVICE, "internal: level capacity exceeded in a host-driven render");
 	}
-	// a device MathException is reported after a complete render (nothing in flight, the
-	// statistics already cleared by k_stats_finish); any other error may leave work queued
-	if (rc && rc != RT_ERR_MATH) {
-		const std::string err = g_error;
-		reset_after_error(s);
-		g_error = err;
-	}
 	return rc;
 }
 
 // The chunks of a render call: every job's selected rows as segments, packed into chunks
 // (render_jobs_impl; rt_debug_plan_chunks exposes it to the CPU tests).
+// pixels of a job's chunks: its chunk_pixels (0: 4 M), at most max_chunk_pixels (> 0: the
+// RTAMD_LEVEL_BUDGET cap, rt_scene::budget_chunk_pixels)
+int64_t chunk_limit(const rt_render_params* p, int64_t max_chunk_pixels) {
+	const int64_t lim = p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22;
+	return max_chunk_pixels > 0 ? std::min(lim, max_chunk_pixels) : lim;
+}
+
 std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size_t n_lanes, bool batch,
-                                              int64_t batch_chunk_pixels, int batch_balance, int chunks_per_lane) {
+                                              int64_t batch_chunk_pixels, int batch_balance, int chunks_per_lane,
+                                              int64_t max_chunk_pixels = 0) {
 	// Pieces: every job's selected rows cut into pieces of at most its chunk size (4 M
 	// pixels by default: it bounds the level buffers); one image over several lanes is cut
 	// so that every lane holds `chunks_per_lane` of its pieces.  Consecutive pieces of
@@ -1667,7 +1785,7 @@ std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size
 			const rt_render_params* p = job.p;
 			uniform = uniform && p->width == j0.p->width && p->height == j0.p->height && job.depth == j0.depth &&
 			          job.io == j0.io;
-			limit_px = std::min(limit_px, p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22);
+			limit_px = std::min(limit_px, chunk_limit(p, max_chunk_pixels));
 			total_rows += job.n_rows;
 		}
 		const int64_t lim_rows = (limit_px / j0.W) & ~int64_t(7);
@@ -1701,7 +1819,7 @@ std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size
 		int64_t cur_px = 0, cur_limit = 0;
 		for (const Job& job : jobs) {
 			const rt_render_params* p = job.p;
-			const int64_t limit_px = p->chunk_pixels > 0 ? p->chunk_pixels : (int64_t)1 << 22;
+			const int64_t limit_px = chunk_limit(p, max_chunk_pixels);
 			const int64_t max_rows = std::max<int64_t>(1, limit_px / job.W);
 			const int64_t want = (!batch && n_lanes > 1) ? static_cast<int64_t>(n_lanes) * chunks_per_lane : 1;
 			const int64_t piece = std::min(max_rows, std::max<int64_t>(1, (job.n_rows + want - 1) / want));
@@ -1743,7 +1861,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 		// of one chunk keeps one lane (cut in two, its chunks each pay the level chain's
 		// latency: C3 1.44 vs 1.33 ms, C1 0.17 vs 0.09 ms)
 		const Job& j = jobs.front();
-		const int64_t limit = j.p->chunk_pixels > 0 ? j.p->chunk_pixels : (int64_t)1 << 22;
+		const int64_t limit = chunk_limit(j.p, s->budget_chunk_pixels);
 		const int64_t max_rows = std::max<int64_t>(1, limit / std::max<int64_t>(1, j.W));
 		const int64_t pieces = (j.n_rows + max_rows - 1) / max_rows;
 		n_lanes = pieces > 1 ? 2 : 1;
@@ -1780,7 +1898,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	R.caller = caller;
 	for (size_t k = 0; k < n_lanes; k++) s->lanes[k]->forked = false;
 	const std::vector<std::vector<Segment>> chunks =
-	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, s->batch_balance, chunks_per_lane);
+	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, s->batch_balance, chunks_per_lane, s->budget_chunk_pixels);
 	R.direct_ok = n_lanes == 1 && chunks.size() == 1;
 	size_t next_chunk = 0;
 	std::unique_ptr<rtamd::MarkerRange> trace_range(new rtamd::MarkerRange("rtamd: trace (levels, shading, output)"));
@@ -2006,14 +2124,24 @@ hipError_t copy_to_host(rt_scene* s, void* dst, const void* src, size_t bytes) {
 	return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
 }
 
-// mapped pinned host staging the kernels write the image into (RTAMD_D2H 3)
+// mapped pinned host staging the kernels write the image into (RTAMD_D2H 3), for images of
+// at most kMappedStageMax bytes (f64 + RGB8: a 2560x1600 frame; a 4096^2 f64 image, 400 MB,
+// is copied instead of pinning that much host memory for the scene's lifetime)
+constexpr size_t kMappedStageMax = size_t(128) << 20;
 int ensure_mapped_stage(rt_scene* s, size_t bytes) {
 	if (s->mapped_stage_bytes >= bytes) return RT_OK;
 	if (s->mapped_stage) (void)hipHostFree(s->mapped_stage);
 	s->mapped_stage = s->mapped_stage_dev = nullptr;
 	s->mapped_stage_bytes = 0;
-	HIP_TRY(hipHostMalloc(&s->mapped_stage, std::max<size_t>(bytes, 256), hipHostMallocMapped));
-	HIP_TRY(hipHostGetDevicePointer(&s->mapped_stage_dev, s->mapped_stage, 0));
+	if (hipHostMalloc(&s->mapped_stage, std::max<size_t>(bytes, 256), hipHostMallocMapped) != hipSuccess) {
+		s->mapped_stage = nullptr;
+		return fail(RT_ERR_DEVICE, "hipHostMalloc (mapped image stage) failed");
+	}
+	if (hipHostGetDevicePointer(&s->mapped_stage_dev, s->mapped_stage, 0) != hipSuccess) {
+		(void)hipHostFree(s->mapped_stage);
+		s->mapped_stage = s->mapped_stage_dev = nullptr;
+		return fail(RT_ERR_DEVICE, "hipHostGetDevicePointer (mapped image stage) failed");
+	}
 	s->mapped_stage_bytes = bytes;
 	return RT_OK;
 }
@@ -2099,14 +2227,20 @@ int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint
 	// RTAMD_D2H 3: the kernels write the image straight into mapped pinned host memory (no
 	// copy engine: its first use in a process costs ~16 ms), then a host memcpy
 	const size_t f64_bytes = out_rgb ? static_cast<size_t>(n) * 3 * sizeof(double) : 0, u8_bytes = out_rgb8 ? static_cast<size_t>(n) * 3 : 0;
+	// Images above kMappedStageMax, or a failed pinned allocation, take the copy path instead:
+	// the scene never holds more than that much pinned host memory for it.
 	char* mapped = nullptr;
-	if (s->d2h_mode == 3 && (rc = ensure_mapped_stage(s, f64_bytes + u8_bytes)) == RT_OK && s->mapped_stage) {
-		mapped = static_cast<char*>(s->mapped_stage);
-		char* dev = static_cast<char*>(s->mapped_stage_dev);
-		if (out_rgb) rgb_dev = reinterpret_cast<double*>(dev);
-		if (out_rgb8) rgb8_dev = reinterpret_cast<uint8_t*>(dev + f64_bytes);
+	if (s->d2h_mode == 3 && f64_bytes + u8_bytes <= kMappedStageMax) {
+		if (ensure_mapped_stage(s, f64_bytes + u8_bytes) == RT_OK && s->mapped_stage) {
+			mapped = static_cast<char*>(s->mapped_stage);
+			char* dev = static_cast<char*>(s->mapped_stage_dev);
+			if (out_rgb) rgb_dev = reinterpret_cast<double*>(dev);
+			if (out_rgb8) rgb8_dev = reinterpret_cast<uint8_t*>(dev + f64_bytes);
+		} else {
+			(void)hipGetLastError();  // the failed allocation is not the render's error: copy_to_host below
+			g_error.clear();
+		}
 	}
-	if (rc) return rc;
 	const double t0 = now_s();
 	rc = render_batch(s, 1, p, &rgb_dev, &rgb8_dev, nullptr, counters, &pr);
 	if (rc) return rc;

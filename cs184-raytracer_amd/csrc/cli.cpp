@@ -170,10 +170,12 @@ double now_ms() {
 	return std::chrono::duration<double, std::milli>(clk::now().time_since_epoch()).count();
 }
 
-// host milliseconds of the run's phases (--timing)
+// host milliseconds of the run's phases (--timing): the top-level phases are consecutive
+// and add up to main_ms; `detail` holds parts of them (scene_create = scene_build +
+// scene_upload + the rest, render = render_gpu + d2h + the rest), not to be added again
 struct Timing {
 	double start = now_ms(), last = start;
-	std::vector<std::pair<std::string, double>> phases;
+	std::vector<std::pair<std::string, double>> phases, detail;
 	void mark(const char* name) {
 		const double t = now_ms();
 		phases.emplace_back(name, t - last);
@@ -184,7 +186,10 @@ struct Timing {
 		if (!f) return;
 		std::fprintf(f, "{");
 		for (const auto& p : phases) std::fprintf(f, "\"%s_ms\": %.3f, ", p.first.c_str(), p.second);
-		std::fprintf(f, "\"main_ms\": %.3f}\n", last - start);
+		std::fprintf(f, "\"main_ms\": %.3f, \"detail\": {", last - start);
+		for (size_t k = 0; k < detail.size(); k++)
+			std::fprintf(f, "%s\"%s_ms\": %.3f", k ? ", " : "", detail[k].first.c_str(), detail[k].second);
+		std::fprintf(f, "}}\n");
 		std::fclose(f);
 	}
 };
@@ -240,8 +245,8 @@ int main(int argc, char** argv) {
 	if (scene) {
 		rt_scene_info info{};
 		rt_scene_get_info(scene, &info);
-		tm.phases.emplace_back("scene_build", info.build_ms);
-		tm.phases.emplace_back("scene_upload", info.upload_ms);
+		tm.detail.emplace_back("scene_build", info.build_ms);
+		tm.detail.emplace_back("scene_upload", info.upload_ms);
 	}
 	tm.mark("scene_create");
 	rt_render_params p{};
@@ -265,8 +270,8 @@ int main(int argc, char** argv) {
 	                       : rt_render(scene, &p, img.data(), update_progress, nullptr, &cnt);
 	set_alarm(false);
 	if (scene) {
-		tm.phases.emplace_back("render_gpu", cnt.host_ms - cnt.copy_ms);
-		tm.phases.emplace_back("d2h", cnt.copy_ms);
+		tm.detail.emplace_back("render_gpu", cnt.host_ms - cnt.copy_ms);
+		tm.detail.emplace_back("d2h", cnt.copy_ms);
 	}
 	tm.mark("render");
 	if (rc == RT_ERR_MATH) {

@@ -76,7 +76,8 @@ class rt_scene_info(ctypes.Structure):
     _fields_ = [("n_geometries", ctypes.c_int32), ("n_spheres", ctypes.c_int32), ("n_meshes", ctypes.c_int32),
                 ("n_lights", ctypes.c_int32), ("n_faces", ctypes.c_int64), ("n_bvh_nodes", ctypes.c_int64),
                 ("device_bytes", ctypes.c_int64), ("max_bvh_depth", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("level_bytes", ctypes.c_int64), ("build_ms", ctypes.c_double), ("upload_ms", ctypes.c_double)]
+                ("level_bytes", ctypes.c_int64), ("build_ms", ctypes.c_double), ("upload_ms", ctypes.c_double),
+                ("level_bytes_peak", ctypes.c_int64), ("level_budget", ctypes.c_int64)]
 
 
 class rt_xform_desc(ctypes.Structure):
@@ -128,6 +129,7 @@ RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AMBIENT = 0, 1, 2
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 
 _lib: Optional[ctypes.CDLL] = None
+RTAMD_ABI_VERSION = 5  # include/rtamd.h
 
 
 def lib() -> ctypes.CDLL:
@@ -179,6 +181,11 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
+    # the ctypes structs above mirror include/rtamd.h of this ABI version
+    L.rt_abi_version.restype, L.rt_abi_version.argtypes = i32, []
+    if L.rt_abi_version() != RTAMD_ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI version {L.rt_abi_version()}, this binding expects "
+                          f"{RTAMD_ABI_VERSION} (include/rtamd.h RTAMD_ABI_VERSION): rebuild it")
     _lib = L
     return L
 

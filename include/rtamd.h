@@ -31,6 +31,13 @@
 extern "C" {
 #endif
 
+/* The layout version of the structs below.  Round 4 appended fields to rt_scene_info
+ * (level_bytes, build_ms, upload_ms) and rt_counters (host_ms, copy_ms): a caller built
+ * against an older header would have those bytes written past its structs.  Check
+ * rt_abi_version() == RTAMD_ABI_VERSION once after loading the library. */
+#define RTAMD_ABI_VERSION 5
+int rt_abi_version(void);
+
 enum {
 	RT_OK = 0,
 	RT_ERR_PARSE = -1,   /* ParseException (exceptions.h:6-21): "line N: ..." / "file not found: ..." */
@@ -63,6 +70,11 @@ typedef struct rt_scene_info {
 	                            (grown on demand, kept for later renders)              */
 	double  build_ms;        /* host time of rt_scene_create's LBVH build + flattening  */
 	double  upload_ms;       /* host time of its HBM allocations, copies and set-up     */
+	int64_t level_bytes_peak;  /* most level-buffer HBM held at once so far (a host-driven
+	                              trace sizes levels with one level of lookahead; after the
+	                              call they are cut back to the rays the levels held)   */
+	int64_t level_budget;    /* RTAMD_LEVEL_BUDGET (0: none): level_bytes never exceeds it;
+	                            a render that would need more is traced in smaller chunks */
 } rt_scene_info;
 
 /* ---------------------------------------------------------------- flat scene descriptor */
@@ -225,9 +237,10 @@ int rt_render_rgb8(rt_scene* s, const rt_render_params* p, uint8_t* out_rgb8,
 
 /* Same, with outputs in device memory (either may be NULL): out_rgb_dev (n_rows*W*3
  * doubles) and out_rgb8_dev (n_rows*W*3 bytes, writers.cpp:4-9 quantisation fused).
- * `stream` is a hipStream_t (NULL = the null stream, or the scene's own stream with
- * RTAMD_SCENE_STREAM=1); the call returns when
- * the work on it is complete. */
+ * `stream` is a hipStream_t; NULL = the scene's own non-blocking stream (the default).
+ * Opt-in exceptions: RTAMD_SCENE_STREAM=0 makes that stream at the scene's second call (the
+ * null stream until then), =2 always uses the null stream.  The call returns when the work
+ * on the stream is complete. */
 int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev,
                      uint8_t* out_rgb8_dev, void* stream, rt_counters* counters);
 

@@ -40,7 +40,9 @@ def cli_run(scene, w, h, flags, runs):
             walls.append((time.perf_counter() - t0) * 1e3)
             phases.append(json.load(open(os.path.join(d, "t.json"))))
     k = walls.index(statistics.median_low(walls))
-    return round(walls[k], 2), {n: round(v, 3) for n, v in phases[k].items()}
+    flat = {n: v for n, v in phases[k].items() if n != "detail"}
+    flat.update({"detail." + n: v for n, v in phases[k].get("detail", {}).items()})
+    return round(walls[k], 2), {n: round(v, 3) for n, v in flat.items()}
 
 
 def main():
