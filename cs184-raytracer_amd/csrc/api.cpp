@@ -103,9 +103,10 @@ struct LevelBuffers {
 
 // A chunk shape traced once host-driven becomes a plan: the same launch sequence with every
 // level size read on the device (k_closest's n from the previous level's child counter,
-// the shading batches and reductions from the hit and child counters), captured once into
-// a hipGraph and replayed for every later chunk of that shape with one hipGraphLaunch.
-// A frame's launches then cost the host one call instead of ~70.  Levels and
+// the shading batches and reductions from the hit and child counters), issued at once for
+// every later chunk of that shape, with no host round trip between levels.
+// (Capturing that sequence into a hipGraph measured slower on this ROCm: graph replay
+// serialised the branches and the lanes; round 2.)  Levels and
 // capacities come from the traced chunk; a replay that would need more (a deeper level, a
 // larger level) is caught on the device (DERR_PLAN, nothing written past a buffer) and the
 // render is redone host-driven.
@@ -139,7 +140,6 @@ struct Plan {
 	// scene), not the host-driven trace's one-level-lookahead bounds
 	std::vector<int64_t> capacity;
 	int launches[3] = {0, 0, 0};
-	hipGraphExec_t exec = nullptr;
 };
 
 // One render pipeline: its own level buffers, streams and events, tracing one chunk of
@@ -204,8 +204,8 @@ struct Lane {
 	std::vector<int64_t> level_n;         // ray counts of the levels known so far
 	std::vector<int> shaded;                        // first level of each shading launch
 	std::vector<std::pair<int, int64_t>> deferred;  // (level, hits) shaded after the chain
-	// launch plans (hipGraphs) of the chunk shapes this lane has traced; invalid once a level
-	// buffer is reallocated
+	// launch plans of the chunk shapes this lane has traced (plain data: the level buffers are
+	// read from the lane when a plan is issued)
 	std::vector<Plan> plans;
 	const Plan* planned = nullptr;        // the plan replaying the current chunk, if any
 	bool forked = false;                  // this call's caller stream joined into the lane's streams
@@ -213,8 +213,6 @@ struct Lane {
 };
 
 void clear_plans(Lane& ln) {
-	for (Plan& p : ln.plans)
-		if (p.exec) (void)hipGraphExecDestroy(p.exec);
 	ln.plans.clear();
 	ln.planned = nullptr;
 }
@@ -236,13 +234,7 @@ struct rt_scene {
 	double* out_dev = nullptr;                   // staging for rt_render (f64)
 	int64_t out_capacity = 0;
 	uint8_t* out8_dev = nullptr;                 // staging for rt_render_rgb8
-	void* host_stage = nullptr;                  // pinned host staging of the image copy (RTAMD_D2H 2)
-	size_t host_stage_bytes = 0;
-	// RTAMD_D2H (copy_to_host, render_to_host): 3, the kernels write the host image into mapped
-	// pinned memory: the CLI's image copy 13-17 ms -> 0.2-2.2 ms (profiles/round4/ab/cli_startup_ab.txt)
-	int d2h_mode = 3;
-	int scene_stream = 1;                        // a stream of its own from the second call on (render_batch)
-	void* mapped_stage = nullptr;                // mapped pinned host image (RTAMD_D2H 3)
+	void* mapped_stage = nullptr;                // mapped pinned host image (render_to_host)
 	void* mapped_stage_dev = nullptr;
 	size_t mapped_stage_bytes = 0;
 	int64_t out8_capacity = 0;
@@ -263,20 +255,14 @@ struct rt_scene {
 	int prio_low = 0, prio_high = 0;
 	int chunks_per_lane = 2;
 	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
-	// RTAMD_FUSE_SHADE: all-lights k_shadow levels shade in place; 2: the per-lane ones of
-	// scenes whose meshes have no LBVH too (C5 21.92 -> 20.50 ms)
-	int fuse_shade = 2;
-	// RTAMD_GRAPH: launch plans of traced chunk shapes: 0 off (every chunk host-driven), 1
-	// replayed as hipGraphs, 2 issued directly (default: this ROCm's graph replay serialises
-	// the branches and the lanes)
-	int graphs = 2;
+	// launch plans of traced chunk shapes (false while a call whose plan missed is redone
+	// host-driven, render_jobs_once)
+	bool plans = true;
 	int64_t batch_chunk_pixels = (int64_t)1 << 22;  // RTAMD_BATCH_CHUNK: most pixels of a chunk packed from several jobs
-	int batch_balance = 1;                       // RTAMD_BATCH_BALANCE: equal chunks, a multiple of the lanes
-	// launch plans without graphs (RTAMD_GRAPH 2) are plain data: a lane adopts a plan another
-	// lane built (growing its level buffers to the plan's capacities) instead of tracing the
-	// chunk shape host-driven itself
+	// plans are plain data: a lane adopts a plan another lane built (growing its level buffers
+	// to the plan's capacities) instead of tracing the chunk shape host-driven itself (+0.7%
+	// whole frames, +1.3% on the 4-way share, round 2)
 	std::vector<Plan> shared_plans;
-	int plan_share = 1;                          // RTAMD_PLAN_SHARE
 	bool force_work_stats = false;               // RTAMD_WORK_STATS: every call counts (rt_render_params::work_stats)
 	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
 	int shadow_all_lights = 3;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
@@ -293,8 +279,9 @@ struct rt_scene {
 	int64_t light_major_below_batch = (int64_t)1 << 17;
 	// RTAMD_ONE_STREAM_PIXELS: a replayed chunk of at most this many pixels is issued on one
 	// stream (Render::issue_plan)
+	// (a plan of one traced level is issued on one stream too: it has no deeper level for its
+	// shading to overlap; C4 0.365 -> 0.351 ms, round 3)
 	int64_t one_stream_pixels = (int64_t)1 << 17;
-	int one_stream_level1 = 1;  // RTAMD_ONE_STREAM_LEVEL1: a plan of one traced level on one stream too
 	// RTAMD_FUSED: a replayed one-stream chunk traces every level in ONE launch (k_fused: closest
 	// hits + shadow rays + Phong terms, and for a plan of one level the output pixels too)
 	// instead of k_closest + k_shadow (+ k_shade) per level and k_output
@@ -311,13 +298,6 @@ struct rt_scene {
 	int64_t level_budget = 0;
 	int64_t budget_chunk_pixels = 0;
 	int64_t calls = 0;            // render calls so far
-	int first_call_minimal = 1;   // RTAMD_FIRST_CALL_MINIMAL: the first call makes no streams (Lane::minimal)
-	int merge_joins = 1;    // RTAMD_MERGE_JOINS: the chain waits for the side shading with one event
-	int launch_events = 1;  // RTAMD_LAUNCH_EVENTS: the chain's events recorded by its launches (hipExtLaunchKernel)
-	// RTAMD_DIRECT: a call of one replayed one-stream chunk runs on the caller's stream itself
-	// (no fork/join across queues) and its last kernel finishes the statistics (no
-	// k_stats_finish launch)
-	int direct = 1;
 	uint32_t* fin_done = nullptr;  // device: blocks done of a launch that finishes the statistics (9 x 128 B)
 	int all_lights_for(int first_level, int64_t hits, int64_t light_major_below) const {
 		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
@@ -379,18 +359,6 @@ struct UploadBatch {
 	}
 };
 
-template <typename T>
-int upload(rt_scene* s, const std::vector<T>& host, const T** dev) {
-	*dev = nullptr;
-	if (host.empty()) return RT_OK;
-	void* p = nullptr;
-	HIP_TRY(hipMalloc(&p, host.size() * sizeof(T)));
-	s->allocs.push_back(p);
-	HIP_TRY(hipMemcpy(p, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
-	s->info.device_bytes += static_cast<int64_t>(host.size() * sizeof(T));
-	*dev = static_cast<const T*>(p);
-	return RT_OK;
-}
 
 // Level buffers grow on demand during a host-driven trace (one level of lookahead: up to
 // four times the rays a level ends up holding), are cut back to what the lane's launch plans
@@ -415,7 +383,6 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
 	const int64_t bytes = level_block_bytes(s, n);
 	if (s->level_budget > 0 && s->info.level_bytes - L.bytes + bytes > s->level_budget) return kBudgetMiss;
-	if (s->graphs == 1) clear_plans(ln);  // captured graphs hold this lane's buffer pointers
 	if (L.block) {
 		HIP_TRY(hipDeviceSynchronize());
 		HIP_TRY(hipFree(L.block));
@@ -599,7 +566,7 @@ struct Render {
 
 	// a replayed chunk of this plan is issued on one stream (issue_plan)
 	bool one_stream(const Lane& ln, const Plan& pl) const {
-		return ln.n0 <= s->one_stream_pixels || (pl.n_levels == 1 && s->one_stream_level1);
+		return ln.n0 <= s->one_stream_pixels || pl.n_levels == 1;
 	}
 	// its levels are fused launches (k_fused): shaded renders of at most 64 shadow lights,
 	// without the work counters
@@ -661,7 +628,7 @@ struct Render {
 		HIP_TRY(hipStreamWaitEvent(q, ln.level_events[last][1], 0));
 		HIP_TRY(hipEventRecord(ev[2], q));
 		// one level traced all-lights-per-lane: k_shadow computes the Phong terms itself
-		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, s->fuse_shade >= 2);
+		b.fused = nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, true);
 		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) cnt.stage_launches[1]++;
 		HIP_TRY(hipEventRecord(ev[3], q));
@@ -690,7 +657,7 @@ struct Render {
 	}
 
 	Plan* find_plan(Lane& ln, const PlanKey& k) const {
-		if (!s->graphs || s->serial) return nullptr;
+		if (!s->plans || s->serial) return nullptr;
 		for (Plan& p : ln.plans)
 			if (p.key == k) return &p;
 		return nullptr;
@@ -718,7 +685,7 @@ struct Render {
 		// grid sizes from the traced chunk's hits (at least one block: the kernels stride)
 		b.shadow_begin[b.n] = std::max<int64_t>(so, 64);
 		b.shade_begin[b.n] = std::max<int64_t>(ho, 64);
-		b.fused = s->fuse_shade && nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, s->fuse_shade >= 2);
+		b.fused = nl > 0 && nl <= 64 && rtamd::shadow_can_fuse(s->ds, b, s->packet_mask, true);
 		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) pl.launches[1]++;
 		if (!b.fused) {
@@ -732,22 +699,14 @@ struct Render {
 	// (no host round trip between levels): the same streams and dependencies as the
 	// host-driven schedule: the chain on ln.stream, direct levels' shading on shade[L % 3]
 	// as soon as their k_closest is done, the deep levels in batches on shade[3] after the
-	// chain, then reductions and the output.  capture: recorded into a graph (with events
-	// of its own; the row table it reads is rewritten for every chunk).
-	int issue_plan(Lane& ln, Plan& pl, bool capture, hipStream_t st, bool finish) {
+	// chain, then reductions and the output.
+	int issue_plan(Lane& ln, Plan& pl, hipStream_t st, bool finish) {
 		const int nlev = pl.n_levels, depth = ln.depth;
 		int rc = RT_OK;
-		std::vector<hipEvent_t> tmp;
-		if (!capture && (rc = ensure_events(ln, nlev))) return rc;
+		if ((rc = ensure_events(ln, nlev))) return rc;
 		// event slots as in the host-driven schedule: [L][1] k_closest(L) done, [L][4] the
 		// shading launch starting at level L done
-		auto ev = [&](int L, int k) -> hipEvent_t {
-			if (!capture) return ln.level_events[L][k];
-			hipEvent_t e = nullptr;
-			if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-			tmp.push_back(e);
-			return e;
-		};
+		auto ev = [&](int L, int k) -> hipEvent_t { return ln.level_events[L][k]; };
 		auto step = [&](hipError_t e) {
 			if (e != hipSuccess && rc == RT_OK) rc = fail(RT_ERR_DEVICE, std::string("planned launch: ") + hipGetErrorString(e));
 		};
@@ -760,7 +719,7 @@ struct Render {
 		// large chunk's overlap of shading and tracing is worth them, a small one's is not.
 		// A plan of one traced level (no bounce: bdepth 0, or nothing reflective was hit) has
 		// nothing to overlap either: C2a 0.185 -> 0.179, C2b 0.334 -> 0.327, C4 0.357 -> 0.355 ms,
-		// C4 2-way share 0.302 -> 0.290 ms (RTAMD_ONE_STREAM_LEVEL1)
+		// C4 2-way share 0.302 -> 0.290 ms (round 3)
 		// the statistics finish inside the last launch (finish: a call of this one chunk): every
 		// block counts itself done (per-XCD counters, trace.hip last_block_finish)
 		rtamd::FusedOut fin{};
@@ -825,11 +784,11 @@ struct Render {
 				const bool last = L == nlev - 1;
 				const int64_t bound = L == 0 ? ln.n0 : std::max<int64_t>(pl.level_n[L], 1);
 				// k_closest(L) done: only the side shading of a direct level waits on it; the
-				// launch records it itself (no marker packet in the chain; not under capture)
+				// launch records it itself (no marker packet in the chain: ~7 us between two kernels)
 				const bool waited = L < direct_levels && !last;
 				hipEvent_t done = waited ? ev(L, 1) : nullptr;
 				if (waited && !done) step(hipErrorOutOfMemory);
-				const bool by_launch = done && s->launch_events && !capture;
+				const bool by_launch = done != nullptr;
 				step(rtamd::launch_closest(s->ds, ln.fg, L, bound, L == 0 ? nullptr : ln.levels[L - 1].lv.counts + 1,
 				                           remaining, ln.levels_dev, s->ctr, s->stats, st, s->packet_mask,
 				                           last && remaining > 0, by_launch ? done : nullptr));
@@ -869,8 +828,8 @@ struct Render {
 		}
 		// the chain joins the side shading once: the last side stream waits for the others (off
 		// the chain's path, long after they finished) and records again; each wait in the chain's
-		// queue costs ~5 us (not under capture: one event recorded twice)
-		if (joins.size() > 1 && s->merge_joins && !capture && rc == RT_OK) {
+		// queue costs ~5 us
+		if (joins.size() > 1 && rc == RT_OK) {
 			const auto last_join = joins.back();
 			for (size_t k = 0; k + 1 < joins.size() && rc == RT_OK; k++)
 				if (joins[k].second != last_join.second) step(hipStreamWaitEvent(last_join.second, joins[k].first, 0));
@@ -886,12 +845,11 @@ struct Render {
 			step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
 			                          st, s->ctr, finish_on(ln.n0, 256) ? &fin : nullptr));
 		for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
-		for (hipEvent_t e : tmp) (void)hipEventDestroy(e);
 		return rc;
 	}
 
 	// A plan for the chunk just traced host-driven (its shape: ln.fg, ln.n0, the job's
-	// depth; its levels: ln.level_n); with RTAMD_GRAPH=1 also captured into a hipGraph.
+	// depth; its levels: ln.level_n), kept by the lane and shared with the others
 	int build_plan(Lane& ln) {
 		Plan pl;
 		pl.key = key_of(ln);
@@ -900,44 +858,27 @@ struct Render {
 		for (int L = 0; L < pl.n_levels; L++) pl.hits.push_back(ln.counts_host[2 * L]);
 		for (int L = 0; L < pl.n_levels; L++) pl.capacity.push_back(std::max<int64_t>(pl.level_n[L], 1));
 		if (s->plan_truncate && pl.n_levels > 1) pl.n_levels--;  // test hook: a plan that must miss
-		if (s->graphs == 1) {
-			hipGraph_t graph = nullptr;
-			HIP_TRY(hipStreamBeginCapture(ln.stream, hipStreamCaptureModeThreadLocal));
-			int rc = issue_plan(ln, pl, true, ln.stream, false);
-			const hipError_t ec = hipStreamEndCapture(ln.stream, &graph);
-			if (rc == RT_OK && ec != hipSuccess)
-				rc = fail(RT_ERR_DEVICE, std::string("hipStreamEndCapture: ") + hipGetErrorString(ec));
-			if (rc == RT_OK && hipGraphInstantiate(&pl.exec, graph, nullptr, nullptr, 0) != hipSuccess)
-				rc = fail(RT_ERR_DEVICE, "hipGraphInstantiate failed");
-			if (graph) (void)hipGraphDestroy(graph);
-			if (rc) return rc;
-		}
 		keep_plan(ln, pl);
-		if (s->graphs == 2) {
-			bool known = false;
-			for (const Plan& q : s->shared_plans) known = known || q.key == pl.key;
-			if (!known) {
-				if (s->shared_plans.size() >= kMaxPlans) s->shared_plans.erase(s->shared_plans.begin());
-				s->shared_plans.push_back(pl);
-			}
+		bool known = false;
+		for (const Plan& q : s->shared_plans) known = known || q.key == pl.key;
+		if (!known) {
+			if (s->shared_plans.size() >= kMaxPlans) s->shared_plans.erase(s->shared_plans.begin());
+			s->shared_plans.push_back(pl);
 		}
 		return RT_OK;
 	}
 
 	// a lane keeps its kMaxPlans most recent plans (called while it replays none)
 	static void keep_plan(Lane& ln, const Plan& pl) {
-		if (ln.plans.size() >= kMaxPlans) {
-			if (ln.plans.front().exec) (void)hipGraphExecDestroy(ln.plans.front().exec);
-			ln.plans.erase(ln.plans.begin());
-		}
+		if (ln.plans.size() >= kMaxPlans) ln.plans.erase(ln.plans.begin());
 		ln.plans.push_back(pl);
 	}
 
-	// A plan of this chunk's shape built by another lane (RTAMD_GRAPH 2), made this lane's
-	// own: its level buffers grown to the plan's capacities
+	// A plan of this chunk's shape built by another lane, made this lane's own: its level
+	// buffers grown to the plan's capacities
 	Plan* adopt_plan(Lane& ln, const PlanKey& k, int& rc) {
 		rc = RT_OK;
-		if (s->graphs != 2 || s->serial || !s->plan_share) return nullptr;
+		if (!s->plans || s->serial) return nullptr;
 		for (const Plan& q : s->shared_plans) {
 			if (!(q.key == k)) continue;
 			// (and the level past the last: its k_closest clears that level's counts)
@@ -955,7 +896,6 @@ struct Render {
 	// now on the device (copy_rows, on the stream the chunk runs on)
 	int prepare_rows(Lane& ln, const std::vector<Segment>& segs, int64_t n_rows, bool* copy) {
 		if (ln.rows_cap < n_rows) {
-			clear_plans(ln);  // graphs hold the table's address
 			if (ln.rows_dev) HIP_TRY(hipFree(ln.rows_dev));
 			if (ln.rows_pin) HIP_TRY(hipHostFree(ln.rows_pin));
 			ln.rows_dev = nullptr;
@@ -994,7 +934,6 @@ struct Render {
 		*copy = !same;
 		ln.rows_uploaded = n_rows;
 		ln.fg.rows = ln.rows_dev;
-		if (s->graphs == 1) return RT_OK;  // captured graphs hold the one table's address
 		// the content's table among the lane's cached ones, else a new (or the least recently
 		// used) one takes it; *copy then says whether that table must be uploaded
 		uint64_t hc = 1469598103934665603ull;
@@ -1064,7 +1003,7 @@ struct Render {
 		// the call's only chunk, replaying a plan of this lane's own: its chain runs on the
 		// caller's stream (no fork, no join; side streams wait on its events as before);
 		// otherwise on the lane's streams after the fork
-		ln.direct = s->direct && direct_ok && pl && !pl->exec;
+		ln.direct = direct_ok && pl;
 		const hipStream_t st = ln.direct ? caller : ln.stream;
 		if (!ln.direct && (rc = fork(ln))) return rc;
 		if (copy_rows)
@@ -1079,12 +1018,8 @@ struct Render {
 		if (pl) {
 			if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
 			// the call's only chunk finishes the statistics in its last kernel (pinned summary)
-			const bool finish = direct_ok && !pl->exec && s->summary_mapped;
-			if (pl->exec) {
-				HIP_TRY(hipGraphLaunch(pl->exec, st));
-			} else if ((rc = issue_plan(ln, *pl, false, st, finish))) {
-				return rc;
-			}
+			const bool finish = direct_ok && s->summary_mapped;
+			if ((rc = issue_plan(ln, *pl, st, finish))) return rc;
 			stats_fused = stats_fused || (finish && finished);
 			HIP_TRY(hipEventRecord(ln.chunk_done, st));
 			ln.planned = pl;
@@ -1160,7 +1095,7 @@ struct Render {
 		}
 		if (ln.call_need.size() < ln.level_n.size()) ln.call_need.resize(ln.level_n.size(), 0);
 		for (size_t L = 0; L < ln.level_n.size(); L++) ln.call_need[L] = std::max(ln.call_need[L], ln.level_n[L]);
-		if (s->graphs && !s->serial && !find_plan(ln, key_of(ln))) {
+		if (s->plans && !s->serial && !find_plan(ln, key_of(ln))) {
 			const int rc = build_plan(ln);
 			if (rc) return rc;
 		}
@@ -1465,66 +1400,39 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	if (const char* nl = std::getenv("RTAMD_LANES")) s->single_lanes = std::min(kMaxLanes, std::max(0, std::atoi(nl)));
 	if (const char* bl = std::getenv("RTAMD_BATCH_LANES"))
 		s->batch_lanes = std::min(kMaxLanes, std::max(1, std::atoi(bl)));
-	if (const char* cp = std::getenv("RTAMD_CHUNKS_PER_LANE")) s->chunks_per_lane = std::max(1, std::atoi(cp));
 	if (const char* se = std::getenv("RTAMD_SERIAL")) s->serial = std::atoi(se);
 	if (const char* al = std::getenv("RTAMD_SHADOW_ALL_LIGHTS")) s->shadow_all_lights = std::atoi(al);
 	if (const char* lm = std::getenv("RTAMD_LIGHT_MAJOR_BELOW"))
 		s->light_major_below_single = s->light_major_below_batch = std::atoll(lm);
 	if (const char* os = std::getenv("RTAMD_ONE_STREAM_PIXELS")) s->one_stream_pixels = std::atoll(os);
-	if (const char* o1 = std::getenv("RTAMD_ONE_STREAM_LEVEL1")) s->one_stream_level1 = std::atoi(o1);
 	if (const char* fu = std::getenv("RTAMD_FUSED")) s->fused = std::atoi(fu);
 	if (const char* fm = std::getenv("RTAMD_FUSED_MIN_PIXELS")) s->fused_min_pixels = std::atoll(fm);
-	if (const char* le = std::getenv("RTAMD_LAUNCH_EVENTS")) s->launch_events = std::atoi(le);
-	if (const char* mj = std::getenv("RTAMD_MERGE_JOINS")) s->merge_joins = std::atoi(mj);
-	if (const char* fm = std::getenv("RTAMD_FIRST_CALL_MINIMAL")) s->first_call_minimal = std::atoi(fm);
-	if (const char* dm = std::getenv("RTAMD_D2H")) s->d2h_mode = std::atoi(dm);
-	if (const char* di = std::getenv("RTAMD_DIRECT")) s->direct = std::atoi(di);
-	if (const char* ds = std::getenv("RTAMD_DEEP_SPLIT"))
-		s->deep_split_single = s->deep_split_batch = std::max(0, std::atoi(ds));
-	if (const char* fs = std::getenv("RTAMD_FUSE_SHADE")) s->fuse_shade = std::atoi(fs);
-	if (const char* gr = std::getenv("RTAMD_GRAPH")) s->graphs = std::atoi(gr);
 	if (const char* pt = std::getenv("RTAMD_PLAN_TRUNCATE")) s->plan_truncate = std::atoi(pt);
 	if (const char* bc = std::getenv("RTAMD_BATCH_CHUNK")) s->batch_chunk_pixels = std::max<int64_t>(1, std::atoll(bc));
-	if (const char* bb = std::getenv("RTAMD_BATCH_BALANCE")) s->batch_balance = std::atoi(bb);
-	if (const char* ps = std::getenv("RTAMD_PLAN_SHARE")) s->plan_share = std::atoi(ps);
 	if (const char* lb = std::getenv("RTAMD_LEVEL_BUDGET")) s->level_budget = std::max<int64_t>(0, std::atoll(lb));
 	s->info.level_budget = s->level_budget;
 	HIP_TRY(hipDeviceGetStreamPriorityRange(&s->prio_low, &s->prio_high));
-	// The scene's own non-blocking stream (work issued without a caller stream).  RTAMD_SCENE_STREAM
-	// 0: the set-up and first call on the null stream and the stream made at the second call
-	// (CLI set-up 32 -> 24 ms), but C3's later single frames then take 1.281 instead of 1.214 ms
-	// (profiles/round4/ab/latency_scene_stream*.txt); 2: always the null stream
-	const char* ss = std::getenv("RTAMD_SCENE_STREAM");
-	s->scene_stream = ss ? std::atoi(ss) : 1;
-	if (s->scene_stream == 1) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-	s->scene_stream = s->scene_stream != 2;
+	// The scene's own non-blocking stream (work issued without a caller stream), made here: on
+	// the null stream until the second call, C3's later single frames took 1.281 instead of
+	// 1.214 ms (round 4, profiles/round4/ab/latency_scene_stream*.txt)
+	HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
 	HIP_TRY(hipEventCreateWithFlags(&s->fork_event, hipEventDisableTiming));
 	int rc;
-	const char* um = std::getenv("RTAMD_UPLOAD");
-	const bool batched = !um || std::atoi(um) != 0;
 	UploadBatch ub;
 	std::vector<rtamd::DCamera> cam(1, fs.camera);
 	std::vector<int32_t> shadow_light;  // j-th non-ambient light -> light index (any number of lights, as scene.cpp:77-108)
 	for (size_t li = 0; li < fs.lights.size(); li++)
 		if (fs.lights[li].kind != rtamd::LIGHT_AMBIENT) shadow_light.push_back(static_cast<int32_t>(li));
-	if (batched) {
-		ub.add(fs.geoms, &s->ds.geoms);
-		ub.add(fs.materials, &s->ds.mats);
-		ub.add(fs.lights, &s->ds.lights);
-		ub.add(fs.face_geo, &s->ds.fgeo);
-		ub.add(fs.face_nrm, &s->ds.fnrm);
-		ub.add(fs.nodes, &s->ds.nodes);
-		ub.add(fs.shadow_order, &s->ds.shadow_order);
-		ub.add(cam, &s->ds.cam);
-		ub.add(shadow_light, &s->ds.shadow_light);
-		rc = ub.commit(s.get());
-	} else {
-		(rc = upload(s.get(), fs.geoms, &s->ds.geoms)) || (rc = upload(s.get(), fs.materials, &s->ds.mats)) ||
-		    (rc = upload(s.get(), fs.lights, &s->ds.lights)) || (rc = upload(s.get(), fs.face_geo, &s->ds.fgeo)) ||
-		    (rc = upload(s.get(), fs.face_nrm, &s->ds.fnrm)) || (rc = upload(s.get(), fs.nodes, &s->ds.nodes)) ||
-		    (rc = upload(s.get(), fs.shadow_order, &s->ds.shadow_order)) || (rc = upload(s.get(), cam, &s->ds.cam)) ||
-		    (rc = upload(s.get(), shadow_light, &s->ds.shadow_light));
-	}
+	ub.add(fs.geoms, &s->ds.geoms);
+	ub.add(fs.materials, &s->ds.mats);
+	ub.add(fs.lights, &s->ds.lights);
+	ub.add(fs.face_geo, &s->ds.fgeo);
+	ub.add(fs.face_nrm, &s->ds.fnrm);
+	ub.add(fs.nodes, &s->ds.nodes);
+	ub.add(fs.shadow_order, &s->ds.shadow_order);
+	ub.add(cam, &s->ds.cam);
+	ub.add(shadow_light, &s->ds.shadow_light);
+	rc = ub.commit(s.get());
 	if (rc) {
 		rt_scene_destroy(s.release());
 		return rc;
@@ -1569,7 +1477,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	                      hipHostMallocDefault));
 	{
 		void* mapped = nullptr;
-		if (!std::getenv("RTAMD_SUMMARY_COPY") && hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
+		if (hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
 			s->summary_mapped = static_cast<unsigned long long*>(mapped);
 		(void)hipGetLastError();
 	}
@@ -1597,7 +1505,6 @@ void rt_scene_destroy(rt_scene* s) {
 	for (void* p : s->allocs) (void)hipFree(p);
 	if (s->out_dev) (void)hipFree(s->out_dev);
 	if (s->out8_dev) (void)hipFree(s->out8_dev);
-	if (s->host_stage) (void)hipHostFree(s->host_stage);
 	if (s->mapped_stage) (void)hipHostFree(s->mapped_stage);
 	if (s->summary_host) (void)hipHostFree(s->summary_host);
 	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
@@ -1662,7 +1569,6 @@ constexpr int64_t kMinBudgetChunkPixels = 1 << 14;
 // host-driven trace (up to four times a level's rays) are not kept between calls.  C5 held
 // 59 GiB of level buffers after one frame in round 4 (missing 3).
 int right_size_levels(rt_scene* s) {
-	if (s->graphs == 1) return RT_OK;  // captured graphs hold the buffers' addresses
 	for (auto& lp : s->lanes) {
 		Lane& ln = *lp;
 		if (!ln.grew) continue;
@@ -1743,11 +1649,10 @@ int render_jobs_once(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 		reset_after_error(s);
 		for (auto& ln : s->lanes) clear_plans(*ln);
 		s->shared_plans.clear();
-		const int graphs = s->graphs;
-		s->graphs = 0;
+		s->plans = false;
 		if (progress) progress->done = 0;
 		rc = render_jobs_impl(s, jobs, caller, counters, progress);
-		s->graphs = graphs;
+		s->plans = true;
 		if (rc == kPlanMiss) rc = fail(RT_ERR_DEVICE, "internal: level capacity exceeded in a host-driven render");
 	}
 	return rc;
@@ -1851,7 +1756,7 @@ std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size
 int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
                      Progress* progress) {
 	const bool batch = jobs.size() > 1;
-	const bool minimal = !batch && s->calls == 0 && s->first_call_minimal && s->lanes.empty() && s->single_lanes == 0;
+	const bool minimal = !batch && s->calls == 0 && s->lanes.empty() && s->single_lanes == 0;
 	s->calls++;
 	size_t n_lanes = batch ? std::min<size_t>(jobs.size(), s->batch_lanes) : static_cast<size_t>(s->single_lanes);
 	int chunks_per_lane = s->chunks_per_lane;
@@ -1898,7 +1803,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	R.caller = caller;
 	for (size_t k = 0; k < n_lanes; k++) s->lanes[k]->forked = false;
 	const std::vector<std::vector<Segment>> chunks =
-	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, s->batch_balance, chunks_per_lane, s->budget_chunk_pixels);
+	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, 1, chunks_per_lane, s->budget_chunk_pixels);
 	R.direct_ok = n_lanes == 1 && chunks.size() == 1;
 	size_t next_chunk = 0;
 	std::unique_ptr<rtamd::MarkerRange> trace_range(new rtamd::MarkerRange("rtamd: trace (levels, shading, output)"));
@@ -2097,34 +2002,15 @@ int ensure_staging(rt_scene* s, int64_t n_pixels, bool f64, bool u8) {
 	return RT_OK;
 }
 
-// The image to the caller's (pageable) host memory.  RTAMD_D2H: 0 hipMemcpy (the runtime
-// stages pageable copies itself); 1 the destination pinned for the copy (hipHostRegister);
-// 2 through pinned staging the scene keeps, then memcpy
-hipError_t copy_to_host(rt_scene* s, void* dst, const void* src, size_t bytes) {
-	if (s->d2h_mode == 1) {
-		if (hipHostRegister(dst, bytes, hipHostRegisterDefault) == hipSuccess) {
-			const hipError_t e = hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
-			(void)hipHostUnregister(dst);
-			return e;
-		}
-	} else if (s->d2h_mode == 2) {
-		if (s->host_stage_bytes < bytes) {
-			if (s->host_stage) (void)hipHostFree(s->host_stage);
-			s->host_stage = nullptr;
-			s->host_stage_bytes = 0;
-			if (hipHostMalloc(&s->host_stage, bytes, hipHostMallocDefault) != hipSuccess) s->host_stage = nullptr;
-			else s->host_stage_bytes = bytes;
-		}
-		if (s->host_stage) {
-			const hipError_t e = hipMemcpy(s->host_stage, src, bytes, hipMemcpyDeviceToHost);
-			if (e == hipSuccess) std::memcpy(dst, s->host_stage, bytes);
-			return e;
-		}
-	}
+// The image to the caller's (pageable) host memory when it is not written into mapped
+// memory (render_to_host): hipMemcpy stages pageable copies itself.  Pinning the destination
+// for the copy, or staging through pinned memory the scene keeps, measured no faster
+// (round 4, profiles/round4/ab/cli_startup_ab.txt).
+hipError_t copy_to_host(void* dst, const void* src, size_t bytes) {
 	return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
 }
 
-// mapped pinned host staging the kernels write the image into (RTAMD_D2H 3), for images of
+// mapped pinned host staging the kernels write the image into, for images of
 // at most kMappedStageMax bytes (f64 + RGB8: a 2560x1600 frame; a 4096^2 f64 image, 400 MB,
 // is copied instead of pinning that much host memory for the scene's lifetime)
 constexpr size_t kMappedStageMax = size_t(128) << 20;
@@ -2158,9 +2044,7 @@ int render_batch(rt_scene* s, int n, const rt_render_params* params, double* con
 		if (rc) return rc;
 	}
 	HIP_TRY(hipSetDevice(s->device));
-	// no caller stream: the scene's (RTAMD_SCENE_STREAM 0: made at the second call)
-	if (!stream_v && !s->stream && s->calls > 0 && s->scene_stream)
-		HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+	// no caller stream: the scene's own
 	hipStream_t caller = stream_v ? static_cast<hipStream_t>(stream_v) : s->stream;
 	// the traversal kernels' instantiation: with the work counters only when asked for
 	s->ds.work_stats = s->force_work_stats;
@@ -2224,13 +2108,14 @@ int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint
 	if (progress) progress(0, pr.total, user);
 	double* rgb_dev = (out_rgb || p->intersection_only) ? s->out_dev : nullptr;
 	uint8_t* rgb8_dev = out_rgb8 ? s->out8_dev : nullptr;
-	// RTAMD_D2H 3: the kernels write the image straight into mapped pinned host memory (no
-	// copy engine: its first use in a process costs ~16 ms), then a host memcpy
+	// the kernels write the image straight into mapped pinned host memory (no copy engine: its
+	// first use in a process costs ~16 ms; the CLI's image copy 13-17 -> 0.2-2.2 ms,
+	// profiles/round4/ab/cli_startup_ab.txt), then a host memcpy
 	const size_t f64_bytes = out_rgb ? static_cast<size_t>(n) * 3 * sizeof(double) : 0, u8_bytes = out_rgb8 ? static_cast<size_t>(n) * 3 : 0;
 	// Images above kMappedStageMax, or a failed pinned allocation, take the copy path instead:
 	// the scene never holds more than that much pinned host memory for it.
 	char* mapped = nullptr;
-	if (s->d2h_mode == 3 && f64_bytes + u8_bytes <= kMappedStageMax) {
+	if (f64_bytes + u8_bytes <= kMappedStageMax) {
 		if (ensure_mapped_stage(s, f64_bytes + u8_bytes) == RT_OK && s->mapped_stage) {
 			mapped = static_cast<char*>(s->mapped_stage);
 			char* dev = static_cast<char*>(s->mapped_stage_dev);
@@ -2250,8 +2135,8 @@ int render_to_host(rt_scene* s, const rt_render_params* p, double* out_rgb, uint
 		if (out_rgb) std::memcpy(out_rgb, mapped, f64_bytes);
 		if (out_rgb8) std::memcpy(out_rgb8, mapped + f64_bytes, u8_bytes);
 	} else {
-		if (out_rgb) HIP_TRY(copy_to_host(s, out_rgb, s->out_dev, f64_bytes));
-		if (out_rgb8) HIP_TRY(copy_to_host(s, out_rgb8, s->out8_dev, u8_bytes));
+		if (out_rgb) HIP_TRY(copy_to_host(out_rgb, s->out_dev, f64_bytes));
+		if (out_rgb8) HIP_TRY(copy_to_host(out_rgb8, s->out8_dev, u8_bytes));
 	}
 	if (counters) {
 		counters->copy_ms = (now_s() - t_copy) * 1e3;

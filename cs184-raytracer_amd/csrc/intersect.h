@@ -207,7 +207,23 @@ __device__ __forceinline__ uint32_t prof_t() {
 #ifndef RT_DIAG_GEOMS
 #define RT_DIAG_GEOMS 0
 #endif
-#if RT_PHASE_PROF || RT_DIAG_LANES || RT_DIAG_GEOMS
+// RT_DIAG_PACKET (diagnostic build, tools/packet_census.py): wave events of the packet
+// searches, [2k] 64 x the waves, [2k + 1] the lanes taking part; k (PacketSlot): shadow
+// (kAnyHit) node iterations, face tests and the stages of the predicated face test a wave
+// gets through, LBVH entries, geometries entered, light verdicts; then the closest-hit ones
+#ifndef RT_DIAG_PACKET
+#define RT_DIAG_PACKET 0
+#endif
+enum PacketSlot : int {
+	PK_NODE = 0, PK_FACE, PK_FACE_FACING, PK_FACE_DA, PK_FACE_DB, PK_FACE_DT, PK_FACE_CAND, PK_BVH, PK_GEOM, PK_LIGHT,
+	PK_C_NODE, PK_C_FACE, PK_C_CAND, PK_C_BVH, PK_C_GEOM, PK_C_ITEM
+};
+#if RT_DIAG_PACKET
+#define DIAG_PK(k, p) diag_lanes(2 * (k), (p))
+#else
+#define DIAG_PK(k, p) ((void)0)
+#endif
+#if RT_PHASE_PROF || RT_DIAG_LANES || RT_DIAG_GEOMS || RT_DIAG_PACKET
 // RT_PHASE_PROF: [stage * 2 + packet][slot] shader cycles; RT_DIAG_LANES (diagnostic build):
 // lane occupancy of the per-lane kernels, read by tools/lane_census.py
 __device__ unsigned long long g_phase[4 * kPhaseSlots];
@@ -271,8 +287,11 @@ __device__ __forceinline__ bool quotient_surely_above(double num, double den, do
 // errs by < 5e-7 |c|_1, and tau = r + 2 (1e-5 max |n_i|_1 + 1e-6 |c|_1) (bvh.cpp
 // facing_data) leaves every dot(n_i, d) beyond 1e-5 |n_i|_1 with the sign of dot(c, d).
 // tau = +inf disables the face's test, a NaN compares false: never a rejection.
+__device__ __forceinline__ float facing_dot(float c0, float c1, float c2, V3 d) {
+	return fmaf(c2, static_cast<float>(d.z), fmaf(c1, static_cast<float>(d.y), c0 * static_cast<float>(d.x)));
+}
 __device__ __forceinline__ bool facing_rejects(float c0, float c1, float c2, float tau, V3 d, bool reverse) {
-	const float s = fmaf(c2, static_cast<float>(d.z), fmaf(c1, static_cast<float>(d.y), c0 * static_cast<float>(d.x)));
+	const float s = facing_dot(c0, c1, c2, d);
 	// s > tau: front false, rejected unless reverse; s < -tau: front true, rejected if reverse
 	return reverse ? s < -tau : s > tau;
 }
@@ -290,6 +309,9 @@ template <bool kAnyHit, typename WS>
 __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn, bool reverse,
                                           double any_limit, MeshBest& best, WS& ws) {
 	ws.inc(W_TRIS);
+#if RT_DIAG_LANES
+	diag_lanes(kAnyHit ? 12 : 14, true);  // [12]/[14] per-lane face tests (shadow/closest): wave slots, lanes
+#endif
 	const DFaceGeo* F = S.fgeo + f;
 	if (face_facing_rejects(F, d, reverse)) return false;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
@@ -333,54 +355,81 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 // branch).  The branchy form pays exec-mask bookkeeping (s_and_saveexec, s_cbranch_execz,
 // the join) at every exit of every face test, in a kernel whose instruction stream is as
 // much scalar as vector; here a lane that has failed just computes along, its results never
-// selected.  Divisions of failed lanes may see D = 0 (inf/NaN, discarded).  The range tests
-// keep the reference's form (geometry.cpp:93-106: a NaN a, b or t is not rejected there).
-// Returns, per lane, kAnyHit && the face passes within any_limit.
+// selected.  The predicates combine with `&` (evaluated, never branched on: `&&` over an
+// expensive right-hand side compiles to an exec-mask branch and a bool round trip through a
+// VGPR), and the lanes taking part come and go as a wave mask (a scalar), not as a per-lane
+// bool carried through the traversal loop (an i1 loop value costs exec-mask merges on every
+// iteration).  Divisions of failed lanes may see D = 0 (inf/NaN, discarded).  The range
+// tests keep the reference's form (geometry.cpp:93-106: a NaN a, b or t is not rejected).
+// on: the lanes testing the face.  Returns the lanes for which kAnyHit && the face passes
+// within any_limit (their question is answered).
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
+__device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+// The lanes where a comparison holds.  A ballot of one comparison is the comparison's own
+// result mask (v_cmp into an SGPR pair); a ballot of a combined bool costs a select and a
+// compare to rebuild the mask, so predicates are combined as masks (s_and / s_xor).
+#define BAL(c) static_cast<uint64_t>(__ballot(c))
+// quotient_surely_negative / _above as lane masks (all lanes of the wave call them)
+__device__ __forceinline__ uint64_t quotient_surely_negative_m(double num, double den) {
+	return (BAL(num < 0) ^ BAL(den < 0)) & BAL(fabs(num) > fabs(den) * 0x1p-1000);
+}
+__device__ __forceinline__ uint64_t quotient_surely_above_m(double num, double den, double lim) {
+	const double thr = fabs(den) * (lim * 1.001);
+	return ~(BAL(num < 0) ^ BAL(den < 0)) & BAL(thr >= 0x1p-1000) & BAL(fabs(num) > thr);
+}
 template <bool kAnyHit, typename WS>
-__device__ __forceinline__ bool test_face_pred(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn,
-                                               bool reverse, double any_limit, MeshBest& best, WS& ws,
-                                               bool on) {
-	ws.add(W_TRIS, on);
+__device__ __forceinline__ uint64_t test_face_pred(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn,
+                                                   bool reverse, double any_limit, MeshBest& best, WS& ws,
+                                                   uint64_t on) {
+	ws.add(W_TRIS, lane_in(on));
 	const auto F = uniform_ptr(S.fgeo) + f;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	const int32_t id = F->id;
 	const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
 	asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
 	             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
-	bool ok = on && !facing_rejects(c0, c1, c2, tau, d, reverse);
-	if (!wave_any(ok)) return false;
+	const float sf = facing_dot(c0, c1, c2, d);
+	const uint64_t rev = BAL(reverse);  // (loop-invariant)
+	uint64_t ok = on & ~((BAL(sf < -tau) & rev) | (BAL(sf > tau) & ~rev));
+	DIAG_PK(kAnyHit ? PK_FACE : PK_C_FACE, lane_in(on));
+	if (!ok) return 0;
+	if (kAnyHit) DIAG_PK(PK_FACE_FACING, lane_in(ok));
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	const double Da = det3(rhs, vb, nd);
-	ok = ok && D != 0 && !quotient_surely_negative(Da, D) && !quotient_surely_above(Da, D, 1.0);
-	if (!wave_any(ok)) return false;
+	ok &= BAL(D != 0) & ~quotient_surely_negative_m(Da, D) & ~quotient_surely_above_m(Da, D, 1.0);
+	if (!ok) return 0;
+	if (kAnyHit) DIAG_PK(PK_FACE_DA, lane_in(ok));
 	const double a = Da / D;
 	const double Db = det3(va, rhs, nd);
-	ok = ok && !(a < 0 || a > 1) && !quotient_surely_negative(Db, D) && !quotient_surely_above(Db, D, 1.0);
-	if (!wave_any(ok)) return false;
+	ok &= ~BAL(a < 0) & ~BAL(a > 1) & ~quotient_surely_negative_m(Db, D) & ~quotient_surely_above_m(Db, D, 1.0);
+	if (!ok) return 0;
+	if (kAnyHit) DIAG_PK(PK_FACE_DB, lane_in(ok));
 	const double b = Db / D;
 	const double Dt = det3(va, vb, rhs);
 	// dist = t * dn with dn = |d|_3 within a few ulps of 1: t > 1.001 * best * 1.001 cannot win
-	const bool beyond = best.dist < INFINITY && best.dist >= 0x1p-900 && quotient_surely_above(Dt, D, best.dist * 1.001);
-	ok = ok && !(b < 0 || a + b > 1) && !quotient_surely_negative(Dt, D) && !beyond;
-	if (!wave_any(ok)) return false;
+	const uint64_t beyond =
+	    BAL(best.dist < INFINITY) & BAL(best.dist >= 0x1p-900) & quotient_surely_above_m(Dt, D, best.dist * 1.001);
+	ok &= ~BAL(b < 0) & ~BAL(a + b > 1) & ~quotient_surely_negative_m(Dt, D) & ~beyond;
+	if (!ok) return 0;
+	if (kAnyHit) DIAG_PK(PK_FACE_DT, lane_in(ok));
 	const double t = Dt / D;
 	const double dist = t * dn;
-	ok = ok && !(t < 0) && (dist < best.dist || (dist == best.dist && id < best.id));
-	if (!wave_any(ok)) return false;
-	ws.add(W_CANDS, ok);
+	ok &= ~BAL(t < 0) & (BAL(dist < best.dist) | (BAL(dist == best.dist) & BAL(id < best.id)));
+	if (!ok) return 0;
+	DIAG_PK(kAnyHit ? PK_FACE_CAND : PK_C_CAND, lane_in(ok));
+	ws.add(W_CANDS, lane_in(ok));
 	const V3 tn = face_normal<true>(S, f, a, b);
-	const bool front = dot4z(tn, d) < 0;
-	ok = ok && !(!front ^ reverse);
-	if (ok) {
+	// the reference's facing test !(!front ^ reverse) == front ^ reverse, front = dot(tn, d) < 0
+	ok &= BAL(dot4z(tn, d) < 0) ^ BAL(reverse);
+	if (lane_in(ok)) {
 		best.dist = dist;
 		best.face = f;
 		best.id = id;
 		best.a = a;
 		best.b = b;
 	}
-	return kAnyHit && ok && dist < any_limit;
+	return kAnyHit ? ok & BAL(dist < any_limit) : 0;
 }
 
 // Slab test of a padded box; conservative: the interval is widened by a relative 1e-9.
@@ -450,6 +499,18 @@ __device__ __forceinline__ float limit32(double lim, double s) {
 	float f = static_cast<float>(l);
 	if (static_cast<double>(f) < l) f = __uint_as_float(__float_as_uint(f) + (f > 0.0f ? 1u : (f == 0.0f ? 1u : 0xffffffffu)));
 	return f;
+}
+// the lanes whose ray passes slab32 (packet traversal: every lane of the wave calls it)
+template <typename P>
+__device__ __forceinline__ uint64_t slab32_m(P lo, P hi, const Ray32& r, float lim, float& tnear) {
+	const float tx0 = fmaf(lo[0], r.ix, -r.oix), tx1 = fmaf(hi[0], r.ix, -r.oix);
+	const float ty0 = fmaf(lo[1], r.iy, -r.oiy), ty1 = fmaf(hi[1], r.iy, -r.oiy);
+	const float tz0 = fmaf(lo[2], r.iz, -r.oiz), tz1 = fmaf(hi[2], r.iz, -r.oiz);
+	const float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+	const float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+	tnear = tmin;
+	return static_cast<uint64_t>(__ballot(tmax >= tmin)) & static_cast<uint64_t>(__ballot(tmax >= 0.0f)) &
+	       static_cast<uint64_t>(__ballot(tmin <= lim));
 }
 template <typename P>
 __device__ __forceinline__ bool slab32(P lo, P hi, const Ray32& r, float lim, float& tnear) {
@@ -694,6 +755,10 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 		PROF_BEGIN(tw0);
 		const bool wb = world_cull(G, o, winv, found ? prune_limit(best_dist) : INFINITY);
 		PROF_END(ws, PH_WORLD, tw0);
+#if RT_DIAG_LANES
+		diag_lanes(2, true);  // [2] wave slots of the per-lane closest-hit geometry loop, [3] lanes in it
+		diag_lanes(4, wb);    // [4], [5] lanes whose ray enters the geometry's world box
+#endif
 		if (!wb) continue;
 		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
 		PROF_BEGIN(tx);
@@ -791,6 +856,10 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 		PROF_BEGIN(tw0);
 		const bool wb = world_cull(G, o, winv, lim);
 		PROF_END(ws, PH_WORLD, tw0);
+#if RT_DIAG_LANES
+		diag_lanes(20, true);  // [20] wave slots of the per-lane shadow geometry loop, [21] lanes still searching
+		diag_lanes(22, wb);    // [22], [23] lanes whose shadow ray enters the geometry's world box
+#endif
 		if (wb && geom_occludes<kMesh>(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
 	}
 	return false;
@@ -815,25 +884,26 @@ template <bool kAnyHit, int kMesh, typename GP, typename WS>
 __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool reverse, bool on, double any_limit,
                                 double prune_cap, FaceHit& fh, bool& settled, double& found_dist,
                                 int32_t* wstack, WS& ws) {
-	settled = false;
 	const double dn = sqrt(d.x * d.x + (d.y * d.y + d.z * d.z));  // Vector3d::norm
 	const V3 nd = -d;
 	MeshBest best;
 	best.dist = INFINITY;
 	best.face = -1;
 	best.id = 0x7fffffff;
-	bool live = on;
-	if (wave_any(live)) {
+	// lanes still searching, and lanes whose question a face answered (wave masks)
+	uint64_t live = __ballot(on), done = 0;
+	if (live) {
 		if (kMesh < kMeshBvh || G->bvh_root < 0) {
 			PROF_BEGIN(tf);
 			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++) {
-				const bool hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws, live);
-				settled = settled || hitf;
-				live = live && !hitf;
+				const uint64_t h = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws, live);
+				done |= h;
+				live &= ~h;
 			}
 				PROF_END(ws, PH_FACES, tf);
 		} else if (!(RT_DIAG_SKIP & 1)) {
-			ws.add(W_ENTRIES, live);
+			ws.add(W_ENTRIES, lane_in(live));
+			DIAG_PK(kAnyHit ? PK_BVH : PK_C_BVH, lane_in(live));
 			const V3 inv = safe_inv(d);
 			const Ray32 r32 = ray32(G, o, d, inv);
 			float lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);  // changes only with best.dist
@@ -861,18 +931,17 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 			// ballot, no instruction)
 			for (;;) {
 				PROF_BEGIN(tn);
-				ws.add(W_NODES, live);
+				ws.add(W_NODES, lane_in(live));
+				DIAG_PK(kAnyHit ? PK_NODE : PK_C_NODE, lane_in(live));
 				float tn0 = 0, tn1 = 0;
-				const bool s0 = slab32(box[0][0], box[0][1], r32, lim, tn0);
-				const bool s1 = slab32(box[1][0], box[1][1], r32, lim, tn1);
-				const unsigned long long L = __ballot(live);
-				const unsigned long long m0 = __ballot(s0) & L, m1 = __ballot(s1) & L;
-				const unsigned long long both = m0 & m1;
+				const uint64_t m0 = slab32_m(box[0][0], box[0][1], r32, lim, tn0) & live;
+				const uint64_t m1 = slab32_m(box[1][0], box[1][1], r32, lim, tn1) & live;
+				const uint64_t both = m0 & m1;
 				// majority near-first: child 1 first when most lanes that need both see it nearer
 				const bool first = 2 * __popcll(__ballot(tn1 < tn0) & both) > __popcll(both) || m0 == 0;
 				const int32_t f_first = first ? rf1 : rf0, c_first = first ? rc1 : rc0;
 				const int32_t f_second = first ? rf0 : rf1, c_second = first ? rc0 : rc1;
-				const unsigned long long w_first = first ? m1 : m0, w_second = first ? m0 : m1;
+				const uint64_t w_first = first ? m1 : m0, w_second = first ? m0 : m1;
 				PROF_END(ws, PH_NODES, tn);
 				// inner children first, so the node to visit next is known (and its record
 				// requested) before the leaf faces are tested: its memory round trip overlaps
@@ -895,25 +964,26 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 				for (int k = 0; k < 2; k++) {
 					const int32_t cf = k ? f_second : f_first, cc = k ? c_second : c_first;
 					if (cc <= 0 || (RT_DIAG_SKIP & 2)) continue;
-					unsigned long long want = k ? w_second : w_first;
-					if (k == 1 && tested) want &= __ballot(live && (first ? tn0 : tn1) <= lim);
+					uint64_t want = (k ? w_second : w_first) & live;
+					if (k == 1 && tested) want &= __ballot((first ? tn0 : tn1) <= lim);
 					if (!want) continue;
 					PROF_BEGIN(tf);
 					const int32_t f0 = fbase + cf;
 					for (int32_t f = f0; f < f0 + cc; f++) {
-						const bool hitf = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws,
-						                                          __builtin_amdgcn_inverse_ballot_w64(want) && live);
-						settled = settled || hitf;
-						live = live && !hitf;
+						const uint64_t h = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws,
+						                                           want & live);
+						done |= h;
+						live &= ~h;
 					}
 					lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 					tested = true;
 					PROF_END(ws, PH_FACES, tf);
 				}
-				if (next < 0 || !wave_any(live)) break;
+				if (next < 0 || !live) break;
 			}
 		}
 	}
+	settled = lane_in(done);
 	found_dist = best.dist;
 	// the reference's gate (geometry.cpp:72), evaluated only for lanes with a result (see mesh_hit)
 	bool keep = on && best.face >= 0;
@@ -942,6 +1012,7 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 		const bool cand = on && world_cull(G, o, winv, found ? prune_limit(best_dist) : INFINITY);
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
+		DIAG_PK(PK_C_GEOM, cand);
 		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
@@ -993,6 +1064,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 #if RT_DIAG_GEOMS
 		if (k < 16) diag_lanes(2 * k, cand);
 #endif
+		DIAG_PK(PK_GEOM, cand);
 		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);

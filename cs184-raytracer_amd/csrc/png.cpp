@@ -92,15 +92,12 @@ void filter_row(const uint8_t* row, const uint8_t* prev, size_t n, uint8_t* out)
 	}
 }
 
-// host threads for the row filters: the process's CPUs (the GPU box's share is 16), at most
-// RTAMD_PNG_THREADS when set
+// host threads for the row filters: the process's CPUs, at most 16 (the GPU box's share)
 int filter_threads() {
 	int n = 1;
 	cpu_set_t set;
 	if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
-	n = std::min(n, 16);
-	if (const char* e = std::getenv("RTAMD_PNG_THREADS")) n = std::atoi(e);
-	return std::max(1, n);
+	return std::max(1, std::min(n, 16));
 }
 
 // optimize_cmf (pngwutil.c:251-288)

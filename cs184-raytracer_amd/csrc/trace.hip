@@ -284,6 +284,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 #if RT_DIAG_LANES
 	if (!kPacket) diag_lanes(0, active);  // [0] wave slots, [1] active lanes of k_closest<false>
 #endif
+	if (kPacket) DIAG_PK(PK_C_ITEM, active);
 	if (kPacket)
 		hit = closest_hit_packet<kMesh>(S, o, d, inside, active, dist, gi, P, Nobj, stack, ctr, ws);
 	else if (active)
@@ -717,6 +718,7 @@ __device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P,
 	}
 #endif
 	bool occ = false;
+	if (kPacket) DIAG_PK(PK_LIGHT, trace);
 	if (kPacket)
 		occ = occluded_packet<kMesh>(S, P, Ld, rev, dL, trace, stack, ctr, ws);
 	else if (trace)
@@ -775,7 +777,7 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 		h = t - j0 * nh64;
 	}
 	const bool on = h < nh;
-	V3 P = mk(0, 0, 0), N = mk(0, 0, 1);
+	V3 P = mk(0, 0, 0);
 	bool inside = false, zero_mat = false;
 	{
 		// the level's record, read here and again where the verdicts are written (opaque: its
@@ -783,18 +785,24 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		if (on) {
 			P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
-			N = mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
 			const uint8_t fl = cur.hinside[h];
 			inside = fl & 1;
 			zero_mat = fl & 2;
 		}
 	}
+	// the shading normal and the viewing direction are read from the hit record where they are
+	// used (each light's set-up, the Phong terms), not held in registers through the searches
+	auto n_of = [&]() {
+		const auto& cur = *uniform_ptr(opaque(levels) + level);
+		return mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
+	};
+	auto d_of = [&]() {
+		const auto& cur = *uniform_ptr(opaque(levels) + level);
+		return mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
+	};
 	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
 	for (int j = j0; j < j1; j++) {
-		const bool v = light_verdict<kPacket, kMesh>(S, j, P, [&]() { return N; }, inside, zero_mat, on, [&]() {
-			const auto& cur = *uniform_ptr(opaque(levels) + level);
-			return mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
-		}, stack, ctr, stats, ws);
+		const bool v = light_verdict<kPacket, kMesh>(S, j, P, n_of, inside, zero_mat, on, d_of, stack, ctr, stats, ws);
 		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
 		if (B.fused) {
 			verdicts |= static_cast<unsigned long long>(v) << j;
@@ -811,10 +819,12 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	// sphere-only kernel, built for 5 waves, would spill 18)
 	// (with LBVH searches it would spill 26 VGPRs; measured neutral on the batch and C3)
 	constexpr bool kLaneFuse = kMesh == kMeshLinear;
+#if RT_DIAG_LANES
+	if (!kPacket && kLaneFuse && B.fused) diag_lanes(28, on);  // [28] wave slots, [29] lanes shading in place
+#endif
 	if ((kPacket || kLaneFuse) && B.fused && on) {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
-		const V3 dv = mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
-		shade_hit(S, cur, h, P, N, dv, [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
+		shade_hit(S, cur, h, P, n_of(), d_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
 		          glibc_pow_data::kLogTab, glibc_pow_data::kExpTab, ctr);
 	}
 }
@@ -1276,7 +1286,7 @@ hipError_t launch_normalize(int64_t n_values, double* rgb, double max_value, uin
 }
 
 hipError_t read_phase_profile(unsigned long long* out) {
-#if RT_PHASE_PROF || RT_DIAG_LANES || RT_DIAG_GEOMS
+#if RT_PHASE_PROF || RT_DIAG_LANES || RT_DIAG_GEOMS || RT_DIAG_PACKET
 	hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(dev::g_phase), sizeof(dev::g_phase));
 	if (e != hipSuccess) return e;
 	static const unsigned long long zero[4 * kPhaseSlots] = {};

@@ -36,3 +36,22 @@ from rtamd.configs import CONFIGS, option_kwargs  # noqa: E402,F401  (BASELINE.j
 # The reference's shipped renders (outputs/image-0N.png, notes/notes-0N.txt:3)
 SHIPPED = {f"image-0{i}.png": (f"inputs/input-0{i}.rti", 2000 if i == 9 else 1000, 2000 if i == 9 else 1000)
            for i in range(1, 10)}
+
+
+# The suite runs the library's own (production) schedule.  Small test images make every
+# shading launch of a single frame trace light-major (api.cpp light_major_below) and every
+# replayed chunk issue on one stream (one_stream_pixels), so the all-lights, fused-Phong and
+# multi-stream forms the full-size renders use are run explicitly where they matter: with
+# ALL_FORMS (the `schedule` parametrisations: every shipped scene and option set, the fuzz
+# sweep's even seeds, the knob tests).
+ALL_FORMS = {"RTAMD_LIGHT_MAJOR_BELOW": "0", "RTAMD_ONE_STREAM_PIXELS": "0"}
+SCHEDULES = ["production", "all-forms"]
+
+
+def apply_schedule(monkeypatch, schedule):
+    """`schedule`: "production" (the library's defaults) or "all-forms" (ALL_FORMS)."""
+    for k, v in ALL_FORMS.items():
+        if schedule == "all-forms":
+            monkeypatch.setenv(k, v)
+        else:
+            monkeypatch.delenv(k, raising=False)

@@ -4,20 +4,8 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# The GPU tests render small images: with the production threshold every shading launch there
-# would trace light-major (api.cpp light_major_below), and the all-lights and fused-Phong
-# forms the full-size renders use would go untested.  The suite defaults to no threshold;
-# tests that exercise it set it explicitly (test_gpu_fuzz odd seeds, knob tests, the bench
-# batch test).
-os.environ.setdefault("RTAMD_LIGHT_MAJOR_BELOW", "0")
-# likewise the one-stream issue of small replayed chunks (api.cpp one_stream_pixels): off by
-# default so the multi-stream schedule stays covered; odd fuzz seeds and a knob test run it
-os.environ.setdefault("RTAMD_ONE_STREAM_PIXELS", "0")
-os.environ.setdefault("RTAMD_ONE_STREAM_LEVEL1", "0")  # and of plans of one traced level
-# and a scene's first call on its own streams (api.cpp Lane::minimal borrows the scene's stream
-# and shades in the chain's order): most tests render a scene once; the production-schedule
-# tests, odd fuzz seeds and a knob test run the minimal first call
-os.environ.setdefault("RTAMD_FIRST_CALL_MINIMAL", "0")
+# The suite runs the library's own (production) schedule; the non-production forms are
+# explicit parametrisations (cases.py ALL_FORMS, apply_schedule).
 for p in (os.path.join(REPO, "cs184-raytracer_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)

@@ -119,7 +119,7 @@ def _batch_rows_worker(rank, world, port, scene, w, h, bdepth, block, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,block", [(2, 8), (3, 4), (3, 1)])
+@pytest.mark.parametrize("world,block", [(2, 8), (3, 4), (3, 1), (8, 8), (8, 1)])
 def test_batched_row_gather(oracle, world, block):
     """bench.py's partition step: all frames of a step gathered in one collective and
     de-interleaved on rank 0 (row blocks)."""
@@ -139,6 +139,14 @@ def test_batched_row_gather(oracle, world, block):
         assert p.exitcode == 0
     for f in range(3):
         assert np.array_equal(got[f], want * (f + 1))
+
+
+@pytest.mark.parametrize("scene,io,block", [("excess_inputs/refraction3.rti", False, 8), ("inputs/input-02.rti", True, 1)])
+def test_partitioned_frame_world8(oracle, scene, io, block):
+    """The driver's 8-GPU layout (one rank per GPU of a node) over gloo: with 8-row blocks
+    ranks 3-7 of a 23-row frame own no rows, and their empty shares still take part in the
+    gather and in the --intersection-only all-reduce(MAX)."""
+    test_partitioned_frame_equals_single_render(oracle, scene, io, block, 8)
 
 
 @pytest.mark.parametrize("io", [False, True])

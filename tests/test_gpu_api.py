@@ -16,7 +16,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from cases import OPTION_SETS, REPO, SCENES, option_kwargs, scene_files
+from cases import OPTION_SETS, REPO, SCENES, SCHEDULES, apply_schedule, option_kwargs, scene_files
 
 pytestmark = pytest.mark.gpu
 
@@ -128,18 +128,20 @@ def test_many_lights(gpu, oracle, tmp_path):
     s.close()
 
 
-@pytest.mark.parametrize("after,graph", [(0, "1"), (0, "0"), (1, "0"), (3, "0")])
-def test_render_after_a_failed_render_is_exact(gpu, oracle, after, graph, monkeypatch):
+@pytest.mark.parametrize("after,replay", [(0, True), (0, False), (1, False), (3, False)])
+def test_render_after_a_failed_render_is_exact(gpu, oracle, after, replay):
     """A device failure in the middle of a render (injected after `after` closest-hit
     launches; a replayed plan counts as one) returns an error; the scene's next render is
-    complete, bit-exact and counts exactly its own rays (no stale lane, counter or error word)."""
-    monkeypatch.setenv("RTAMD_GRAPH", graph)
+    complete, bit-exact and counts exactly its own rays (no stale lane, counter or error word).
+    replay: the failing render replays a launch plan; else it is the first of its shape
+    (host-driven, level by level)."""
     scene = "excess_inputs/bunny.rti"
     w, h, bdepth = 80, 45, 4
     want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
     s = gpu.load_scene(os.path.join(SCENES, scene))
     o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth)
-    s.renderScene(options=o)  # lanes and level buffers exist
+    # lanes and level buffers exist; with replay, a plan of this shape too
+    s.renderScene(options=o if replay else gpu.Options(renderWidth_=w + 8, renderHeight_=h, bounceDepth_=bdepth))
     s.debug_fail_after(after)
     with pytest.raises(gpu.DeviceError, match="injected"):
         s.renderScene(options=o)
@@ -149,16 +151,15 @@ def test_render_after_a_failed_render_is_exact(gpu, oracle, after, graph, monkey
     s.close()
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
 @pytest.mark.parametrize("scene", ["excess_inputs/bunny.rti", "inputs/input-06.rti"])
-def test_fused_multi_level_shadow_batches(gpu, oracle, scene, fuse, monkeypatch):
+def test_fused_multi_level_shadow_batches(gpu, oracle, scene, monkeypatch):
     """All-lights shadow layout for the deep levels too (SHADOW_ALL_LIGHTS 3), packets for
     every level (PACKET_MASK 63) and one direct level, so deep levels are shaded in
-    multi-level batches with and without the fused Phong terms."""
+    multi-level batches with the fused Phong terms."""
     w, h, bdepth = 72, 40, 6
     want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
     for k, v in (("RTAMD_SHADOW_ALL_LIGHTS", "3"), ("RTAMD_PACKET_MASK", "63"), ("RTAMD_DIRECT_LEVELS", "1"),
-                 ("RTAMD_FUSE_SHADE", fuse)):
+                 ("RTAMD_LIGHT_MAJOR_BELOW", "0")):
         monkeypatch.setenv(k, v)
     s = gpu.load_scene(os.path.join(SCENES, scene))
     img = s.renderScene(options=gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth))
@@ -183,12 +184,13 @@ def test_camera_eye_direction_vector_raises(gpu):
 @pytest.mark.parametrize("scene,bdepth,chunk", [("excess_inputs/bunny.rti", 4, 0), ("excess_inputs/refraction3.rti", 8, 0),
                                                 ("excess_inputs/refraction3.rti", 8, 900), ("inputs/input-06.rti", 10, 0),
                                                 ("inputs/input-09.rti", 10, 1500)])
-@pytest.mark.parametrize("graph", ["0", "1", "2"])
-def test_replayed_plans_are_exact(gpu, oracle, scene, bdepth, chunk, graph, monkeypatch):
-    """Launch plans (hipGraph replay of a traced chunk shape, device-read level sizes): the
-    2nd and 3rd renders of the same shape replay the plan; every render is bit-exact with
-    the oracle and counts the reference's rays."""
-    monkeypatch.setenv("RTAMD_GRAPH", graph)
+@pytest.mark.parametrize("schedule", SCHEDULES)
+def test_replayed_plans_are_exact(gpu, oracle, scene, bdepth, chunk, schedule, monkeypatch):
+    """Launch plans (the launch sequence of a traced chunk shape issued at once, device-read
+    level sizes): the 2nd and 3rd renders of the same shape replay the plan, in level buffers
+    cut back to the plan's ray counts; every render is bit-exact with the oracle and counts
+    the reference's rays."""
+    apply_schedule(monkeypatch, schedule)
     w, h = 90, 50
     want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
     s = gpu.load_scene(os.path.join(SCENES, scene))
@@ -201,12 +203,10 @@ def test_replayed_plans_are_exact(gpu, oracle, scene, bdepth, chunk, graph, monk
     s.close()
 
 
-@pytest.mark.parametrize("graph", ["1", "2"])
-def test_replayed_plan_batch_and_rgb8(gpu, monkeypatch, graph):
+def test_replayed_plan_batch_and_rgb8(gpu):
     """A batch of frames over three lanes (each lane builds, then replays, its plan) with
-    f64 and RGB8 outputs (graph replay: written through the plans' output records)."""
+    f64 and RGB8 outputs."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("RTAMD_GRAPH", graph)
     scene = "excess_inputs/bunny.rti"
     s = gpu.load_scene(os.path.join(SCENES, scene))
     w, h = 96, 54
@@ -223,15 +223,15 @@ def test_replayed_plan_batch_and_rgb8(gpu, monkeypatch, graph):
     s.close()
 
 
-@pytest.mark.parametrize("graph", ["1", "2"])
+@pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("scene,bdepth,io", [("excess_inputs/refraction3.rti", 8, False), ("inputs/input-05.rti", 10, False),
                                              ("inputs/input-02.rti", 10, True)])
-def test_plan_miss_is_redone_exactly(gpu, oracle, scene, bdepth, io, graph, monkeypatch):
+def test_plan_miss_is_redone_exactly(gpu, oracle, scene, bdepth, io, schedule, monkeypatch):
     """A plan one level short (RTAMD_PLAN_TRUNCATE test hook): its replay raises DERR_PLAN
     on the device instead of writing the unplanned children, and the render is redone
     host-driven: still bit-exact, counters exact."""
     monkeypatch.setenv("RTAMD_PLAN_TRUNCATE", "1")
-    monkeypatch.setenv("RTAMD_GRAPH", graph)
+    apply_schedule(monkeypatch, schedule)
     w, h = 64, 40
     want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth, intersection_only=io)
     s = gpu.load_scene(os.path.join(SCENES, scene))
@@ -244,15 +244,13 @@ def test_plan_miss_is_redone_exactly(gpu, oracle, scene, bdepth, io, graph, monk
 
 
 @pytest.mark.parametrize("pack", ["4194304", "20000", "1"])
-@pytest.mark.parametrize("graph", ["0", "2"])
-def test_multi_frame_chunks(gpu, oracle, pack, graph, monkeypatch):
+def test_multi_frame_chunks(gpu, oracle, pack, monkeypatch):
     """Chunks packed from rows of several frames (consecutive batch entries with equal width,
     height and depth: one GPU's shares of row-partitioned frames, whole frames, chunked
     frames) trace as one wavefront; every entry equals its own render, bit for bit, and the
     summed counters equal the single renders' (RTAMD_BATCH_CHUNK bounds the packing)."""
     torch = pytest.importorskip("torch")
     monkeypatch.setenv("RTAMD_BATCH_CHUNK", pack)
-    monkeypatch.setenv("RTAMD_GRAPH", graph)
     scene = "excess_inputs/refraction3.rti"
     w, h, bd = 70, 44, 7
     want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bd)
@@ -285,13 +283,11 @@ def test_multi_frame_chunks(gpu, oracle, pack, graph, monkeypatch):
     s.close()
 
 
-@pytest.mark.parametrize("graph", ["2", "1"])
-def test_work_counters_are_optional(gpu, monkeypatch, graph):
+def test_work_counters_are_optional(gpu, monkeypatch):
     """rt_render_params.work_stats selects the counting instantiation of the traversal
     kernels: the same bits either way, the traversal counters nonzero only when asked for
-    (RTAMD_WORK_STATS=1 asks for every call); plans and graphs keyed on it."""
+    (RTAMD_WORK_STATS=1 asks for every call); plans keyed on it."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("RTAMD_GRAPH", graph)
     w, h = 96, 64
     s = gpu.load_scene(os.path.join(SCENES, "excess_inputs/bunny.rti"))
     outs = {}

@@ -14,6 +14,8 @@ import os
 import numpy as np
 import pytest
 
+from cases import apply_schedule
+
 pytestmark = pytest.mark.gpu
 
 
@@ -104,12 +106,7 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
     # odd seeds: the production light-major threshold (every launch here is below it);
     # RTAMD_FUZZ_PRODUCTION=1: every seed under the library's own defaults (and rendered twice)
     production = seed % 2 or os.environ.get("RTAMD_FUZZ_PRODUCTION") == "1"
-    for knob in ("RTAMD_LIGHT_MAJOR_BELOW", "RTAMD_ONE_STREAM_PIXELS", "RTAMD_ONE_STREAM_LEVEL1",
-                 "RTAMD_FIRST_CALL_MINIMAL"):
-        if production:
-            monkeypatch.delenv(knob, raising=False)
-        else:
-            monkeypatch.setenv(knob, "0")
+    apply_schedule(monkeypatch, "production" if production else "all-forms")
     path, bdepth, io = random_scene(seed, tmp_path)
     w, h = _W, _H
     try:

@@ -17,6 +17,7 @@ cfg = sys.argv[2] if len(sys.argv) > 2 else "C3_bunny_1920x1080_bd4"
 scene, w, h, flags = CONFIGS[cfg]
 kw = option_kwargs(flags)
 s = rtamd.load_scene(os.path.join(SCENES, scene))
+s.upload()
 L = rtamd.lib()
 L.rt_debug_phase_profile.restype = ctypes.c_int
 L.rt_debug_phase_profile.argtypes = [ctypes.c_int, ctypes.c_void_p]
@@ -29,6 +30,13 @@ for _ in range(frames):
     s.render_device(prm, out.data_ptr())
 L.rt_debug_phase_profile(0, buf)
 rows = [(0, "k_closest<false>: active lanes per wave slot"),
+        (2, "k_closest<false>: lanes in the geometry loop per iteration"),
+        (4, "k_closest<false>: lanes entering a geometry (world box hit) per iteration"),
+        (14, "k_closest<false>: lanes in a linear face test"),
+        (12, "k_shadow<false>: lanes in a linear face test"),
+        (20, "k_shadow<false>: lanes still searching per geometry iteration"),
+        (22, "k_shadow<false>: lanes entering a geometry (world box hit) per iteration"),
+        (28, "k_shadow<false>: lanes shading in place (per-lane fused Phong)"),
         (8, "k_closest<false>: lanes entering an LBVH search per wave entering"),
         (10, "k_closest<false>: lanes holding a leaf per face phase"),
         (16, "k_shadow<false>: lanes with a hit per wave slot"),
