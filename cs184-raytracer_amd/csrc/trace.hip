@@ -728,103 +728,6 @@ __device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P,
 	return occ || zero;
 }
 
-// Per-lane shadow verdicts of lights [j0, j1) for scenes without LBVHs (kMesh < kMeshBvh),
-// geometry-major: the any-hit over the geometries (scene.cpp:87-93, castRay scene.cpp:142-167;
-// an `any`, so order-free) runs with the geometry outside and the lane's rays inside.  Per
-// geometry (wave-uniform, its record in SGPRs) every lane culls each of its pending rays
-// against the geometry's world box, then takes its candidate rays one at a time: a lane
-// whose ray towards light 0 misses the geometry tests its ray towards light 1 in the same
-// step, so the geometry's test (object-space transform, normalisation, sphere or face test)
-// runs for the lanes with ANY candidate ray instead of, light after light, for the few lanes
-// whose one ray enters it.  The light-outer loop ran that test with 9% of the lanes on C5
-// (profiles/round5/census/lane_census_c5.txt).  Lights go in groups of kGmLights; each
-// pending ray's direction and light distance wait in LDS (park: kGmLights x 4 doubles per
-// lane, strided by the block size), its facing flag in a bit mask.
-#ifndef RT_GM_LIGHTS
-#define RT_GM_LIGHTS 4
-#endif
-constexpr int kGmLights = RT_GM_LIGHTS;
-template <int kMesh, typename NV, typename DV, typename WS>
-__device__ __forceinline__ unsigned long long lane_verdicts(const DeviceScene& S, int j0, int j1, V3 P, NV n_of,
-                                                            bool inside, bool zero_mat, bool on, DV dv_of,
-                                                            int32_t* stack, DeviceCounters* ctr,
-                                                            unsigned long long* stats, WS& ws, lds_f64* park) {
-	unsigned long long verdicts = 0;
-	lds_f64* pk = park + threadIdx.x;
-	// ray q of the group: [4q] .. [4q + 2] direction, [4q + 3] light distance (stride kBlock)
-	auto ray_of = [&](int q, V3& d, double& dl) {
-		const lds_f64* r = opaque_lds(pk) + 4 * q * kBlock;
-		d = mk(r[0], r[kBlock], r[2 * kBlock]);
-		dl = r[3 * kBlock];
-	};
-	for (int g0 = j0; g0 < j1; g0 += kGmLights) {
-		const int n = min(kGmLights, j1 - g0);
-		uint32_t pending = 0;  // bit q: the ray towards light g0 + q is traced and not yet occluded
-		uint32_t revs = 0;     // bit q: its facing flag (castRay's `reverse`)
-		for (int q = 0; q < n; q++) {
-			bool zero = false;
-			if (on) {  // light_verdict's set-up
-				const V3 N = n_of();
-				const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[g0 + q]);
-				const bool point = L.kind == DLIGHT_POINT;
-				const V3 lv = load3(L.vec);
-				const V3 Ld = ray_dir(point ? lv - P : -lv, ctr);  // Light::calculateRayToLight
-				const double nl_dot = dot4z(N, Ld);
-				if ((nl_dot < 0) ^ inside) revs |= 1u << q;
-				const double dL = point ? sqrt(sq4(lv - P)) : INFINITY;
-				if (zero_mat && L.zero_terms && nl_dot <= 0.0) {
-					const V3 R = (2 * nl_dot) * N - Ld;
-					zero = -dot4z(dv_of(), R) <= 0.0;
-				}
-				// the reference's castRay maps every ray into every object space (may raise)
-				check_may_raise(S, Ld, true, ctr);
-				lds_f64* r = pk + 4 * q * kBlock;
-				r[0] = Ld.x, r[kBlock] = Ld.y, r[2 * kBlock] = Ld.z, r[3 * kBlock] = dL;
-				if (!zero) pending |= 1u << q;
-			}
-#if RT_DIAG_LANES
-			diag_lanes(16, on);
-			diag_lanes(18, on && !zero);
-#endif
-			const unsigned long long mz = __ballot(zero);
-			if (mz && __lane_id() == 0) atomicAdd(shard(stats) + ST_SHADOW_ZERO, (unsigned long long)__popcll(mz));
-			if (zero) verdicts |= 1ull << (g0 + q);
-		}
-		for (int k = 0; k < S.n_geoms && wave_any(pending != 0); k++) {
-			const int g = uniform_ptr(S.shadow_order)[k];
-			const auto G = uniform_ptr(S.geoms) + g;
-			uint32_t cand = 0;
-			for (int q = 0; q < n; q++) {
-				if (!((pending >> q) & 1)) continue;
-				V3 d;
-				double dl;
-				ray_of(q, d, dl);
-				if (world_cull(G, P, safe_inv(d), shadow_slab_limit(dl))) cand |= 1u << q;
-			}
-#if RT_DIAG_LANES
-			diag_lanes(20, pending != 0);
-			diag_lanes(22, cand != 0);
-			diag_any(30, cand != 0);
-#endif
-			while (wave_any(cand != 0)) {
-				const bool has = cand != 0;
-				const int q = has ? __builtin_ctz(cand) : 0;
-				cand &= cand - 1;
-				if (has) {
-					V3 d;
-					double dl;
-					ray_of(q, d, dl);
-					if (geom_occludes<kMesh>(S, G, P, d, (revs >> q) & 1, dl, stack, ctr, ws)) {
-						pending &= ~(1u << q);
-						verdicts |= 1ull << (g0 + q);
-					}
-				}
-			}
-		}
-	}
-	return verdicts;
-}
-
 // A fused level's shading (closest_item<.., kFused>): the verdicts of every light for the
 // hit held in registers, then its Phong terms (scene.cpp:78-108) into col.  on: the lane has
 // a hit to shade (every lane of the wave calls it).
@@ -853,7 +756,7 @@ __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, in
 template <bool kPacket, bool kCount, int kMesh>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
-                                            uint32_t* stat_lds, lds_f64* park) {
+                                            uint32_t* stat_lds) {
 	const int nl = S.n_nonambient;
 	const BatchItem it = batch_item<true>(B, nl, tg);
 	const int level = it.level;
@@ -898,22 +801,14 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 		return mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
 	};
 	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
-	if constexpr (!kPacket && kMesh < kMeshBvh) {
-		verdicts = lane_verdicts<kMesh>(S, j0, j1, P, n_of, inside, zero_mat, on, d_of, stack, ctr, stats, ws, park);
-		if (!B.fused && on) {
+	for (int j = j0; j < j1; j++) {
+		const bool v = light_verdict<kPacket, kMesh>(S, j, P, n_of, inside, zero_mat, on, d_of, stack, ctr, stats, ws);
+		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
+		if (B.fused) {
+			verdicts |= static_cast<unsigned long long>(v) << j;
+		} else if (on) {
 			const auto& cur = *uniform_ptr(opaque(levels) + level);
-			for (int j = j0; j < j1; j++) cur.occl[j * cur.capacity + h] = (verdicts >> j) & 1;
-		}
-	} else {
-		for (int j = j0; j < j1; j++) {
-			const bool v = light_verdict<kPacket, kMesh>(S, j, P, n_of, inside, zero_mat, on, d_of, stack, ctr, stats, ws);
-			// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
-			if (B.fused) {
-				verdicts |= static_cast<unsigned long long>(v) << j;
-			} else if (on) {
-				const auto& cur = *uniform_ptr(opaque(levels) + level);
-				cur.occl[j * cur.capacity + h] = v;
-			}
+			cur.occl[j * cur.capacity + h] = v;
 		}
 	}
 	if (on) PROF_END(ws, PH_TOTAL, t_total);
@@ -943,14 +838,11 @@ __global__ void __launch_bounds__(kBlock)
                                                                      unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
-	// the geometry-major per-lane verdicts' rays (lane_verdicts)
-	__shared__ double gm_park[!kPacket && kMesh < kMeshBvh ? 4 * kGmLights * kBlock : 1];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
-		shadow_item<kPacket, kCount, kMesh>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds,
-		                                    (lds_f64*)gm_park);
+		shadow_item<kPacket, kCount, kMesh>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
