@@ -234,6 +234,14 @@ __device__ __forceinline__ void diag_lanes(int slot, bool p) {
 		atomicAdd(&g_phase[slot + 1], (unsigned long long)__popcll(m));
 	}
 }
+// [slot] 64 x the wave events, [slot + 1] 64 x those in which some lane has p
+__device__ __forceinline__ void diag_any(int slot, bool p) {
+	const unsigned long long m = __ballot(p);
+	if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) {
+		atomicAdd(&g_phase[slot], 64ull);
+		if (m) atomicAdd(&g_phase[slot + 1], 64ull);
+	}
+}
 #endif
 
 // A mesh hit (face, barycentric a, b), or a sphere hit (face -1, ray parameter t in a)
@@ -758,6 +766,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 #if RT_DIAG_LANES
 		diag_lanes(2, true);  // [2] wave slots of the per-lane closest-hit geometry loop, [3] lanes in it
 		diag_lanes(4, wb);    // [4], [5] lanes whose ray enters the geometry's world box
+		diag_any(6, wb);      // [6], [7] iterations in which some lane enters it
 #endif
 		if (!wb) continue;
 		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
@@ -859,6 +868,7 @@ __device__ bool occluded(const DeviceScene& S, V3 o, V3 d, bool reverse, double 
 #if RT_DIAG_LANES
 		diag_lanes(20, true);  // [20] wave slots of the per-lane shadow geometry loop, [21] lanes still searching
 		diag_lanes(22, wb);    // [22], [23] lanes whose shadow ray enters the geometry's world box
+		diag_any(30, wb);      // [30], [31] iterations in which some lane enters it
 #endif
 		if (wb && geom_occludes<kMesh>(S, G, o, d, reverse, dist_light, stack, ctr, ws)) return true;
 	}

@@ -32,10 +32,12 @@ L.rt_debug_phase_profile(0, buf)
 rows = [(0, "k_closest<false>: active lanes per wave slot"),
         (2, "k_closest<false>: lanes in the geometry loop per iteration"),
         (4, "k_closest<false>: lanes entering a geometry (world box hit) per iteration"),
+        (6, "k_closest<false>: iterations in which some lane enters the geometry"),
         (14, "k_closest<false>: lanes in a linear face test"),
         (12, "k_shadow<false>: lanes in a linear face test"),
         (20, "k_shadow<false>: lanes still searching per geometry iteration"),
         (22, "k_shadow<false>: lanes entering a geometry (world box hit) per iteration"),
+        (30, "k_shadow<false>: iterations in which some lane enters the geometry"),
         (28, "k_shadow<false>: lanes shading in place (per-lane fused Phong)"),
         (8, "k_closest<false>: lanes entering an LBVH search per wave entering"),
         (10, "k_closest<false>: lanes holding a leaf per face phase"),
