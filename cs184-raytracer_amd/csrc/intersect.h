@@ -56,13 +56,6 @@ __device__ __forceinline__ const T* opaque(const T* p) {
 	asm volatile("" : "+s"(p));
 	return p;
 }
-// LDS doubles, and an LDS address the compiler cannot see through: values parked there are
-// read back at their uses, not kept in registers from the store
-typedef __attribute__((address_space(3))) double lds_f64;
-__device__ __forceinline__ lds_f64* opaque_lds(lds_f64* p) {
-	asm volatile("" : "+v"(p));
-	return p;
-}
 template <bool kUniform, typename T>
 __device__ __forceinline__ auto scene_ptr(const T* p) {
 	if constexpr (kUniform)
@@ -1063,36 +1056,19 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 }
 
 // Packet form of occluded(): same decisions per lane (see occluded()).
-// park (kPacketParkSlots doubles per lane, strided by the block size): the world ray, its
-// inverse direction and the light distance wait there through the geometries' searches and
-// are read back where each geometry's cull, transform and distance test use them, instead of
-// holding 20 VGPRs through the LBVH traversals (the packet kernels' occupancy is set by their
-// registers: 4 waves per SIMD at 128).
-constexpr int kPacketParkSlots = 10;
 template <int kMesh, typename WS>
-__device__ bool occluded_packet(const DeviceScene& S, V3 o_in, V3 d_in, bool reverse, double dist_in, bool on,
-                                int32_t* wstack, DeviceCounters* ctr, WS& ws, lds_f64* park) {
-	const bool inf_light = dist_in == INFINITY;
+__device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, double dist_light, bool on,
+                                int32_t* wstack, DeviceCounters* ctr, WS& ws) {
+	const bool inf_light = dist_light == INFINITY;
+	const V3 winv = safe_inv(d);
 	bool occ = false;
-	check_may_raise(S, d_in, on, ctr);
+	check_may_raise(S, d, on, ctr);
 	if (RT_DIAG_SKIP & 4) return false;
-	lds_f64* pk = park + threadIdx.x;
-	{
-		const V3 wi = safe_inv(d_in);
-		const double v[kPacketParkSlots] = {o_in.x, o_in.y, o_in.z, d_in.x, d_in.y, d_in.z, wi.x, wi.y, wi.z, dist_in};
-#pragma unroll
-		for (int k = 0; k < kPacketParkSlots; k++) pk[k * kBlock] = v[k];
-	}
-	auto slot3 = [&](int k) {
-		const lds_f64* q = opaque_lds(pk);
-		return mk(q[k * kBlock], q[(k + 1) * kBlock], q[(k + 2) * kBlock]);
-	};
-	auto dist_of = [&]() { return opaque_lds(pk)[9 * kBlock]; };
 	for (int k = 0; k < S.n_geoms; k++) {
 		const int g = uniform_ptr(S.shadow_order)[k];
 		const auto G = uniform_ptr(S.geoms) + g;
 		PROF_BEGIN(tw0);
-		const bool cand = on && !occ && world_cull(G, slot3(0), slot3(6), inf_light ? INFINITY : dist_of() * (1.0 + 1e-6));
+		const bool cand = on && !occ && world_cull(G, o, winv, inf_light ? INFINITY : dist_light * (1.0 + 1e-6));
 		PROF_END(ws, PH_WORLD, tw0);
 		if (!wave_any(cand)) continue;
 #if RT_DIAG_GEOMS
@@ -1100,8 +1076,8 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o_in, V3 d_in, bool rev
 #endif
 		DIAG_PK(PK_GEOM, cand);
 		PROF_BEGIN(tx);
-		const V3 oo = xf_point(G->inv, slot3(0));
-		const V3 draw = xf_dir(G->inv, slot3(3));
+		const V3 oo = xf_point(G->inv, o);
+		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
 		double nrm;
 		const V3 dd = normalized3(draw, &nrm);
@@ -1115,7 +1091,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o_in, V3 d_in, bool rev
 			hit = cand && sphere_hit(G, oo, dd, reverse, h.a);
 		PROF_END(ws, PH_SPHERE, ts);
 		} else {
-			const double tl = inf_light ? INFINITY : dist_of() * nrm;
+			const double tl = inf_light ? INFINITY : dist_light * nrm;
 			const double cap = inf_light ? INFINITY : tl * (1.0 + 1e-7) + 1e-300;
 			hit = mesh_hit_packet<true, kMesh>(S, G, oo, dd, reverse, cand, inf_light ? INFINITY : tl * (1.0 - 1e-7), cap, h,
 			                            settled, fd, wstack, ws);
@@ -1139,7 +1115,7 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o_in, V3 d_in, bool rev
 				occ = true;
 			} else {
 				const V3 Pw = xf_point(G->fwd, hit_point<kMesh>(S, h, oo, dd));
-				if (sqrt(sq4(Pw - slot3(0))) <= dist_of()) occ = true;
+				if (sqrt(sq4(Pw - o)) <= dist_light) occ = true;
 			}
 		}
 	}

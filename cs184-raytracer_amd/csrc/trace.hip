@@ -35,6 +35,13 @@ __device__ __forceinline__ int64_t div_small(int64_t n, int64_t d) {
 }
 
 constexpr int kShadeBlock = 512;
+typedef __attribute__((address_space(3))) double lds_f64;
+// an LDS address the compiler cannot see through: values are read back from LDS, not kept in
+// registers from the store
+__device__ __forceinline__ lds_f64* opaque_lds(lds_f64* p) {
+	asm volatile("" : "+v"(p));
+	return p;
+}
 #ifndef RT_FUSED_PARK
 #define RT_FUSED_PARK 1
 #endif
@@ -64,15 +71,6 @@ constexpr int kWaveStack = kStackDepth;
 // test's registers (at 5 waves the per-lane kernels spill 18-21 VGPRs)
 #ifndef RT_LINEAR_WAVES
 #define RT_LINEAR_WAVES 4
-#endif
-// The packet shadow kernel: its waves per SIMD, and whether it computes the Phong terms of the
-// all-lights levels itself (ShadeBatch::fused) or leaves them to k_shade (whose registers then
-// do not count against the traversal's occupancy)
-#ifndef RT_PACKET_SHADOW_WAVES
-#define RT_PACKET_SHADOW_WAVES RT_PACKET_WAVES
-#endif
-#ifndef RT_PACKET_FUSE_SHADE
-#define RT_PACKET_FUSE_SHADE 1
 #endif
 
 // Camera::calculateViewingRay (rtbase.h:74-84) for pixel (r, c) (scene.cpp:26-30)
@@ -250,7 +248,7 @@ __device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, 
 template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
 __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, NV n_of, DV dir_of,
                                                bool inside, int32_t* stack, DeviceCounters* ctr,
-                                               unsigned long long* stats, WS& ws, double col[3], lds_f64* opark);
+                                               unsigned long long* stats, WS& ws, double col[3]);
 
 // Closest hit (castRay, scene.cpp:142-167) + the bounce decisions of scene.cpp:110-136:
 // the children's rays and the reflective weight depend only on the hit, not on the
@@ -412,11 +410,10 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 				const lds_f64* q = opaque_lds(pk);
 				return mk(q[3 * kBlock], q[4 * kBlock], q[5 * kBlock]);
 			};
-			shade_in_place<kPacket, kMesh>(S, shade, gi, P, n_of, d_of, inside, stack, ctr, stats, ws, col,
-			                               park + 6 * kBlock);
+			shade_in_place<kPacket, kMesh>(S, shade, gi, P, n_of, d_of, inside, stack, ctr, stats, ws, col);
 		} else {
 			shade_in_place<kPacket, kMesh>(S, shade, gi, P, [&]() { return N; }, [&]() { return d; }, inside, stack, ctr,
-			                               stats, ws, col, park);
+			                               stats, ws, col);
 		}
 		if (!active) return;
 		if (fo->final) {
@@ -565,9 +562,7 @@ __global__ void __launch_bounds__(kBlock)
         const RayLevel* levels, DeviceCounters* ctr, unsigned long long* stats, FusedOut fo) {
 	__shared__ AppendLds append_lds;
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
-	// the fused shading's normal and viewing direction (6 doubles per lane), then the shadow
-	// searches' world ray (occluded_packet)
-	__shared__ double park_mem[kPacket ? (6 + kPacketParkSlots) * kBlock : 1];
+	__shared__ double park_mem[RT_FUSED_PARK && kPacket ? 6 * kBlock : 1];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -692,14 +687,13 @@ __device__ __forceinline__ void shade_hit(const DeviceScene& S, const LV& cur, i
 // colour is the same bits whether the light is occluded or not (it is never -0), so that ray
 // is not traced.  dv_of(): the viewing direction, read only for that test.  Every lane of
 // the wave calls it (kPacket: the search is wave-uniform; lanes without a hit pass on false).
-template <bool kPacket, int kMesh, typename PV, typename NV, typename DV, typename WS>
-__device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, PV p_of, NV n_of, bool inside, bool zero_mat,
+template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
+__device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, V3 P, NV n_of, bool inside, bool zero_mat,
                                               bool on, DV dv_of, int32_t* stack, DeviceCounters* ctr,
-                                              unsigned long long* stats, WS& ws, lds_f64* opark) {
+                                              unsigned long long* stats, WS& ws) {
 	V3 Ld = mk(0, 0, 1);
 	bool rev = false, zero = false;
 	double dL = 0;
-	const V3 P = on ? p_of() : mk(0, 0, 0);
 	if (on) {
 		const V3 N = n_of();
 		const auto& L = *(uniform_ptr(S.lights) + uniform_ptr(S.shadow_light)[j]);
@@ -726,7 +720,7 @@ __device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, PV p_
 	bool occ = false;
 	if (kPacket) DIAG_PK(PK_LIGHT, trace);
 	if (kPacket)
-		occ = occluded_packet<kMesh>(S, P, Ld, rev, dL, trace, stack, ctr, ws, opark);
+		occ = occluded_packet<kMesh>(S, P, Ld, rev, dL, trace, stack, ctr, ws);
 	else if (trace)
 		occ = occluded<kMesh>(S, P, Ld, rev, dL, stack, ctr, ws);
 	const unsigned long long mz = __ballot(zero);
@@ -740,13 +734,12 @@ __device__ __forceinline__ bool light_verdict(const DeviceScene& S, int j, PV p_
 template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
 __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, int gi, V3 P, NV n_of, DV dir_of,
                                                bool inside, int32_t* stack, DeviceCounters* ctr,
-                                               unsigned long long* stats, WS& ws, double col[3], lds_f64* opark) {
+                                               unsigned long long* stats, WS& ws, double col[3]) {
 	const bool zero_mat = on && S.mats[S.geoms[gi].mat].zero_terms;
 	unsigned long long verdicts = 0;  // bit j: the j-th non-ambient light's verdict (<= 64 lights)
 	for (int j = 0; j < S.n_nonambient; j++)
 		verdicts |= static_cast<unsigned long long>(
-		                light_verdict<kPacket, kMesh>(S, j, [&]() { return P; }, n_of, inside, zero_mat, on, dir_of, stack, ctr,
-		                                              stats, ws, opark))
+		                light_verdict<kPacket, kMesh>(S, j, P, n_of, inside, zero_mat, on, dir_of, stack, ctr, stats, ws))
 		            << j;
 	if (on)
 		phong(S, gi, P, n_of(), dir_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
@@ -763,7 +756,7 @@ __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, in
 template <bool kPacket, bool kCount, int kMesh>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
-                                            uint32_t* stat_lds, lds_f64* opark) {
+                                            uint32_t* stat_lds) {
 	const int nl = S.n_nonambient;
 	const BatchItem it = batch_item<true>(B, nl, tg);
 	const int level = it.level;
@@ -784,24 +777,21 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 		h = t - j0 * nh64;
 	}
 	const bool on = h < nh;
+	V3 P = mk(0, 0, 0);
 	bool inside = false, zero_mat = false;
 	{
 		// the level's record, read here and again where the verdicts are written (opaque: its
 		// buffer pointers are not held in scalar registers through the traversals)
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		if (on) {
+			P = mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
 			const uint8_t fl = cur.hinside[h];
 			inside = fl & 1;
 			zero_mat = fl & 2;
 		}
 	}
-	// the hit point, the shading normal and the viewing direction are read from the hit record
-	// where they are used (each light's set-up, the Phong terms), not held in registers through
-	// the searches
-	auto p_of = [&]() {
-		const auto& cur = *uniform_ptr(opaque(levels) + level);
-		return mk(cur.hpx[h], cur.hpy[h], cur.hpz[h]);
-	};
+	// the shading normal and the viewing direction are read from the hit record where they are
+	// used (each light's set-up, the Phong terms), not held in registers through the searches
 	auto n_of = [&]() {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		return mk(cur.hnx[h], cur.hny[h], cur.hnz[h]);
@@ -812,7 +802,7 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	};
 	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
 	for (int j = j0; j < j1; j++) {
-		const bool v = light_verdict<kPacket, kMesh>(S, j, p_of, n_of, inside, zero_mat, on, d_of, stack, ctr, stats, ws, opark);
+		const bool v = light_verdict<kPacket, kMesh>(S, j, P, n_of, inside, zero_mat, on, d_of, stack, ctr, stats, ws);
 		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
 		if (B.fused) {
 			verdicts |= static_cast<unsigned long long>(v) << j;
@@ -832,9 +822,9 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 #if RT_DIAG_LANES
 	if (!kPacket && kLaneFuse && B.fused) diag_lanes(28, on);  // [28] wave slots, [29] lanes shading in place
 #endif
-	if (((kPacket && RT_PACKET_FUSE_SHADE) || kLaneFuse) && B.fused && on) {
+	if ((kPacket || kLaneFuse) && B.fused && on) {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
-		shade_hit(S, cur, h, p_of(), n_of(), d_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
+		shade_hit(S, cur, h, P, n_of(), d_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
 		          glibc_pow_data::kLogTab, glibc_pow_data::kExpTab, ctr);
 	}
 }
@@ -843,18 +833,16 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 // strides over the items (the bound is block-uniform: no lane of a wave leaves early).
 template <bool kPacket, bool kCount, int kMesh>
 __global__ void __launch_bounds__(kBlock)
-    __attribute__((amdgpu_waves_per_eu(kMesh == kMeshNone && !kPacket ? RT_SPHERE_WAVES : kMesh == kMeshLinear && !kPacket ? RT_LINEAR_WAVES : kPacket ? (kMesh == kMeshBvh ? RT_PACKET_SHADOW_WAVES : RT_PACKET_WAVES) : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
+    __attribute__((amdgpu_waves_per_eu(kMesh == kMeshNone && !kPacket ? RT_SPHERE_WAVES : kMesh == kMeshLinear && !kPacket ? RT_LINEAR_WAVES : kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
                                                                      unsigned long long* stats) {
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
-	__shared__ double opark_mem[kPacket ? kPacketParkSlots * kBlock : 1];  // occluded_packet's world ray
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
-		shadow_item<kPacket, kCount, kMesh>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds,
-		                                    (lds_f64*)opark_mem);
+		shadow_item<kPacket, kCount, kMesh>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -1194,7 +1182,7 @@ static bool shadow_packet(const ShadeBatch& b, int packet_mask) {
 }
 
 bool shadow_can_fuse(const DeviceScene& s, const ShadeBatch& b, int packet_mask, bool per_lane) {
-	return b.all_lights && ((shadow_packet(b, packet_mask) && RT_PACKET_FUSE_SHADE) || (per_lane && s.mesh_kind == kMeshLinear));
+	return b.all_lights && (shadow_packet(b, packet_mask) || (per_lane && s.mesh_kind == kMeshLinear));
 }
 
 // grid of a device-counted batch: one thread per item of `bound` (an upper bound of its
