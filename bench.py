@@ -490,9 +490,55 @@ def emulated_scaling(a, local, torch):
                                  "rendered alone on this one GPU, one share at a time",
                     "gather_model": f"largest remote share's RGB8 rows / {XGMI_LINK_GBS:g} GB/s per xGMI link + "
                                     f"{XGMI_FIXED_US:g} us (assumed, not measured)",
-                    "curve": curve}
+                    "curve": curve,
+                    "batch_partition_8way": emulated_batch_partition(a, s, W, H, kw, blk, cfg, torch)}
         s.close()
     return out
+
+
+BATCH_FRAMES = {"C5_refraction3_4096_bd8": 16}  # frames per emulated batch step (default 48, bench.py's own)
+
+
+def emulated_batch_partition(a, s, W, H, kw, blk, cfg, torch, n=8):
+    """The throughput form of an n-GPU node for a sweep config (VERDICT r4 "next" 3): every
+    rank renders its row blocks of the SAME F frames in one rt_render_batch_device call (the
+    bench's partition mode), emulated on this one GPU one rank's share at a time; the node's
+    step takes the slowest share (+ the assumed gather of its F x rows of RGB8).  Reported
+    beside the one-GPU batch of the same F whole frames."""
+    from rtamd import dist as rd
+    F = BATCH_FRAMES.get(cfg, 48)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def timed(prm_list, rows):
+        outs = torch.empty((len(prm_list), rows, W, 3), dtype=torch.uint8, device="cuda")
+        ts, rays = [], 0
+        for rep in range(a.sweep_reps + 1):  # rep 0: warm-up (level buffers, launch plans)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            st = s.render_batch_device(prm_list, [], [outs[f].data_ptr() for f in range(len(prm_list))], stream)
+            torch.cuda.synchronize()
+            if rep > 0:
+                ts.append(time.perf_counter() - t0)
+            rays = st.rays
+        return statistics.median(ts) * 1e3, rays
+
+    whole_ms, whole_rays = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)] * F, H)
+    share_ms, rays = [], 0
+    for k in range(n):
+        rows = rd.n_rows(H, k, n, blk)
+        ms, r = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], k * blk, H, n, row_block=blk)] * F, rows)
+        share_ms.append(round(ms, 3))
+        rays += r
+    remote_rows = max(rd.n_rows(H, k, n, blk) for k in range(1, n))
+    gather_ms = F * remote_rows * W * 3 / (XGMI_LINK_GBS * 1e9) * 1e3 + XGMI_FIXED_US / 1e3
+    node_ms = max(share_ms) + gather_ms
+    return {"frames_per_step": F, "n_gpus": n, "one_gpu_batch_ms": round(whole_ms, 3),
+            "one_gpu_mrays_per_s": round(whole_rays / whole_ms / 1e3, 1),
+            "share_ms_per_rank": share_ms, "max_share_ms": max(share_ms),
+            "imbalance": round(max(share_ms) / (sum(share_ms) / n), 3), "gather_ms_assumed": round(gather_ms, 3),
+            "projected_node_mrays_per_s": round(rays / node_ms / 1e3, 1),
+            "projected_speedup": round(whole_ms / node_ms, 3),
+            "per_gpu_mrays_per_s_of_share": round(rays / n / (sum(share_ms) / n) / 1e3, 1)}
 
 
 def strong_scaling(a, world, rank, local, groups, dist, torch):

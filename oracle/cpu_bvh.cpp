@@ -86,6 +86,8 @@ bool hits_bounding_box(V3 o, V3 d, const double* mn, const double* mx) {  // geo
 }
 
 const FlatScene* S;
+// LBVH work of this thread (node visits = nodes whose two child boxes were tested; face tests)
+thread_local long long t_nodes = 0, t_tris = 0;
 
 struct MeshBest {
 	double dist;
@@ -102,6 +104,7 @@ V3 face_normal(int32_t f, double a, double b) {
 
 // geometry.cpp:78-124, one face; same acceptance as intersect.h test_face
 bool test_face(bool any_hit, int32_t f, V3 o, V3 d, V3 nd, double dn, bool reverse, double any_limit, MeshBest& best) {
+	t_tris++;
 	const DFaceGeo& F = S->face_geo[f];
 	const V3 p0 = load3(F.p0), va = load3(F.va), vb = load3(F.vb);
 	const V3 rhs = o - p0;
@@ -158,6 +161,7 @@ bool mesh_search(bool any_hit, const DGeom& G, V3 o, V3 d, bool reverse, double 
 	for (;;) {
 		if (ref >= 0) {
 			const DBvhNode& N = S->nodes[ref];
+			t_nodes++;
 			const double lim = std::fmin(prune_limit(best.dist), prune_cap);
 			double t0, t1;
 			const bool h0 = slab(N.lo[0], N.hi[0], o, inv, lim, t0), h1 = slab(N.lo[1], N.hi[1], o, inv, lim, t1);
@@ -285,6 +289,7 @@ bool occluded(V3 o, V3 d, bool reverse, double dist_light) {
 
 struct Counts {
 	int64_t trace = 0, shadow = 0;
+	long long nodes = 0, tris = 0;
 };
 
 double max0(double x) { return (x < 0.0) ? 0.0 : x; }
@@ -402,6 +407,8 @@ int main(int argc, char** argv) {
 					trace(load3(cam.eye), d, depth, false, &img[(k * W + c) * 3], counts[w]);
 				}
 			}
+			counts[w].nodes = t_nodes;
+			counts[w].tris = t_tris;
 		});
 	for (auto& t : pool) t.join();
 	const auto t2 = std::chrono::steady_clock::now();
@@ -419,9 +426,12 @@ int main(int argc, char** argv) {
 	for (const Counts& c : counts) {
 		tot.trace += c.trace;
 		tot.shadow += c.shadow;
+		tot.nodes += c.nodes;
+		tot.tris += c.tris;
 	}
-	std::printf("{\"trace_rays\": %lld, \"shadow_rays\": %lld, \"render_s\": %.6f, \"setup_s\": %.6f, \"threads\": %d}\n",
-	            static_cast<long long>(tot.trace), static_cast<long long>(tot.shadow),
+	std::printf("{\"trace_rays\": %lld, \"shadow_rays\": %lld, \"node_visits\": %lld, \"tri_tests\": %lld, "
+	            "\"render_s\": %.6f, \"setup_s\": %.6f, \"threads\": %d}\n",
+	            static_cast<long long>(tot.trace), static_cast<long long>(tot.shadow), tot.nodes, tot.tris,
 	            std::chrono::duration<double>(t2 - t1).count(), std::chrono::duration<double>(t1 - t0).count(), threads);
 	return 0;
 }
