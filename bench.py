@@ -126,6 +126,13 @@ def latest_traffic():
     return old if os.path.exists(old) else None
 
 
+def level_buffers(s):
+    inf = s.info()
+    return {"level_bytes": inf.level_bytes, "level_gib": round(inf.level_bytes / 2**30, 3),
+            "level_bytes_peak": inf.level_bytes_peak, "level_peak_gib": round(inf.level_bytes_peak / 2**30, 3),
+            "budget": inf.level_budget}
+
+
 def core_info():
     """The host cores the CPU baseline may use, with the evidence: every
     CPU of this process's affinity set, capped by the cgroup CPU quota when one is set (the
@@ -847,6 +854,9 @@ def main():
             "traversal_work_per_frame": solo["work_per_frame"] if solo else None,
             "strong_scaling": sweep,
             "topology": topology,
+            # HBM the timed scene's level buffers hold after the run, their peak during it, and the
+            # RTAMD_LEVEL_BUDGET they were held to (0: none)
+            "level_buffers": level_buffers(s),
         }
         if res["roofline"]:
             # the dominant kernel's solo time per step must fit in the step (a consistent time base)

@@ -1427,6 +1427,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	ub.add(fs.materials, &s->ds.mats);
 	ub.add(fs.lights, &s->ds.lights);
 	ub.add(fs.face_geo, &s->ds.fgeo);
+	ub.add(fs.face_cone, &s->ds.fcone);
 	ub.add(fs.face_nrm, &s->ds.fnrm);
 	ub.add(fs.nodes, &s->ds.nodes);
 	ub.add(fs.shadow_order, &s->ds.shadow_order);
@@ -2211,6 +2212,17 @@ int rt_debug_phase_profile(int device, unsigned long long* out32) {
 	HIP_TRY(hipDeviceSynchronize());
 	HIP_TRY(rtamd::read_phase_profile(out32));
 	return RT_OK;
+}
+
+// Diagnostic: the per-wave timing records of an RT_DIAG_WAVETIME build (tools/wave_times.py;
+// 32 B each: t0, t1 on the 100 MHz clock, tag, first item, node iterations, face tests), at
+// most max_records, read and cleared; returns the count (0 in other builds).  Not in rtamd.h.
+int rt_debug_wave_times(int device, void* out, int max_records) {
+	HIP_TRY(hipSetDevice(device));
+	HIP_TRY(hipDeviceSynchronize());
+	const int n = rtamd::read_wave_times(out, max_records);
+	if (n < 0) return fail(RT_ERR_DEVICE, "wave time read-back failed");
+	return n;
 }
 
 int rt_selftest_math(int device, int op, const double* x, const double* y, double* out, int64_t n) {

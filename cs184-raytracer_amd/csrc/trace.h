@@ -15,6 +15,7 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DMaterial* mats;
 	const DLight* lights;
 	const DFaceGeo* fgeo;
+	const DFaceCone* fcone;
 	const DFaceNrm* fnrm;
 	const DBvhNode* nodes;
 	const int32_t* shadow_order;              // geometry order of the occlusion query
@@ -195,6 +196,9 @@ hipError_t launch_copy16(void* dst, const void* src, int64_t n_words, hipStream_
 // PhaseSlot); copied and cleared.
 constexpr int kPhaseSlots = 8;
 hipError_t read_phase_profile(unsigned long long* out /* 4 * kPhaseSlots */);
+// RT_DIAG_WAVETIME builds: the wave records since the last call (32 B each, intersect.h
+// WaveTime), at most max_records, then cleared; 0 in other builds, -1 on a HIP error
+int read_wave_times(void* out, int max_records);
 // FETCH_SIZE calibration: reads `bytes` of buf once, `width` (1, 4, 8, 16) bytes per lane
 // VALU issue calibration: kind 0 v_fma_f32, 1 v_pk_fma_f32, 2 v_fma_f64 chains at
 // waves_per_simd waves on every SIMD

@@ -474,8 +474,10 @@ __global__ void __launch_bounds__(kBlock)
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
+		WT_BEGIN();
 		closest_item<kPacket, kCount, kMesh>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
 		                      append_lds, stack, stat_lds);
+		WT_END(1 | kPacket << 4 | level << 8, base + (threadIdx.x & ~63));
 	}
 }
 
@@ -573,10 +575,13 @@ __global__ void __launch_bounds__(kBlock)
 	}
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride)
+	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
+		WT_BEGIN();
 		closest_item<kPacket, false, kMesh, true>(S, fg, level, n, remaining, plan_last, levels, ctr, stats,
 		                                          base + threadIdx.x, append_lds, stack, nullptr, &fo,
 		                                          (lds_f64*)(park_mem));
+		WT_END(2 | kPacket << 4 | level << 8, base + (threadIdx.x & ~63));
+	}
 	if (fo.summary) last_block_finish(stats, ctr, fo);
 }
 
@@ -841,8 +846,11 @@ __global__ void __launch_bounds__(kBlock)
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-	for (int64_t base = xcd_block() * kBlock; base < total; base += stride)
+	for (int64_t base = xcd_block() * kBlock; base < total; base += stride) {
+		WT_BEGIN();
 		shadow_item<kPacket, kCount, kMesh>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
+		WT_END(3 | kPacket << 4 | B.level[0] << 8, base + (threadIdx.x & ~63));
+	}
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
@@ -1294,6 +1302,23 @@ hipError_t read_phase_profile(unsigned long long* out) {
 #else
 	for (int k = 0; k < 4 * kPhaseSlots; k++) out[k] = 0;
 	return hipSuccess;
+#endif
+}
+
+int read_wave_times(void* out, int max_records) {
+#if RT_DIAG_WAVETIME
+	unsigned int n = 0;
+	if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(dev::g_wt_n), sizeof(n)) != hipSuccess) return -1;
+	n = std::min<unsigned int>(n, dev::kWaveTimes);
+	const int m = std::min<int>(static_cast<int>(n), max_records);
+	if (m > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(dev::g_wt), m * sizeof(dev::WaveTime)) != hipSuccess) return -1;
+	const unsigned int zero = 0;
+	if (hipMemcpyToSymbol(HIP_SYMBOL(dev::g_wt_n), &zero, sizeof(zero)) != hipSuccess) return -1;
+	return m;
+#else
+	(void)out;
+	(void)max_records;
+	return 0;
 #endif
 }
 
