@@ -1427,7 +1427,6 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	ub.add(fs.materials, &s->ds.mats);
 	ub.add(fs.lights, &s->ds.lights);
 	ub.add(fs.face_geo, &s->ds.fgeo);
-	ub.add(fs.face_cone, &s->ds.fcone);
 	ub.add(fs.face_nrm, &s->ds.fnrm);
 	ub.add(fs.nodes, &s->ds.nodes);
 	ub.add(fs.shadow_order, &s->ds.shadow_order);

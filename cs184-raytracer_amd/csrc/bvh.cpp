@@ -237,12 +237,12 @@ bool direction_may_vanish(const Affine& inv) {
 	return !(sigma_min_bound > 4e-12);  // |v|_2 > sqrt(3) 1e-12 with margin for rounding
 }
 
-// Facing pre-test data of a face (DFaceCone): the fp32 mean c of the three vertex
+// Facing pre-test data of a face (DFaceGeo::cone_*): the fp32 mean c of the three vertex
 // normals, their largest distance r from it, and tau = r + 2 (kFacingRel |n|_1 + 1e-6 |c|_1)
 // with |n|_1 the largest normal's 1-norm, rounded up; tau = +inf (no pre-test) when a
 // normal is not finite or zero, or the normals' magnitudes are far apart (the interpolated
 // normal's rounding then scales with the largest one).  intersect.h face_facing_rejects.
-void facing_data(const Face& f, DFaceCone& fg) {
+void facing_data(const Face& f, DFaceGeo& fg) {
 	long double c[3] = {0, 0, 0};
 	double lo = INFINITY, hi = 0;
 	bool ok = true;
@@ -257,21 +257,21 @@ void facing_data(const Face& f, DFaceCone& fg) {
 		hi = std::max(hi, l1);
 	}
 	ok = ok && lo > 1e-30 && hi < 1e30 && hi <= 1e6 * lo;
-	fg.tau = INFINITY;
-	for (int k = 0; k < 3; k++) fg.c[k] = ok ? static_cast<float>(c[k]) : 0.0f;
+	fg.cone_tau = INFINITY;
+	for (int k = 0; k < 3; k++) fg.cone_c[k] = ok ? static_cast<float>(c[k]) : 0.0f;
 	if (!ok) return;
 	long double r = 0, cl1 = 0;
-	for (int k = 0; k < 3; k++) cl1 += std::fabs((long double)fg.c[k]);
+	for (int k = 0; k < 3; k++) cl1 += std::fabs((long double)fg.cone_c[k]);
 	for (int v = 0; v < 3; v++) {
 		long double e = 0;
 		for (int k = 0; k < 3; k++) {
-			const long double x = (long double)f.n[v][k] - fg.c[k];
+			const long double x = (long double)f.n[v][k] - fg.cone_c[k];
 			e += x * x;
 		}
 		r = std::max(r, std::sqrt(e));
 	}
 	const long double tau = (r * (1 + 1e-12L) + 2 * (kFacingRel * hi + 1e-6L * cl1));
-	fg.tau = round_up_f32(static_cast<double>(tau) * (1 + 1e-12));
+	fg.cone_tau = round_up_f32(static_cast<double>(tau) * (1 + 1e-12));
 }
 
 }  // namespace
@@ -374,9 +374,7 @@ FlatScene flatten_scene(const Scene& s) {
 				fn.n1[k] = f.n[1][k];
 				fn.n2[k] = f.n[2][k];
 			}
-			DFaceCone fc;
-			facing_data(f, fc);
-			fs.face_cone.push_back(fc);
+			facing_data(f, fg);
 			fs.face_geo.push_back(fg);
 			fs.face_nrm.push_back(fn);
 			fs.face_geo.back().id = static_cast<int32_t>(local);
@@ -454,8 +452,6 @@ FlatScene flatten_scene(const Scene& s) {
 	};
 	std::stable_sort(fs.shadow_order.begin(), fs.shadow_order.end(),
 	                 [&](int32_t a, int32_t b) { return cost(a) < cost(b); });
-	// the cones of a leaf's faces are read as one block of kLeafFaces records (intersect.h)
-	fs.face_cone.resize(fs.face_geo.size() + kLeafFaces - 1, DFaceCone{{0.0f, 0.0f, 0.0f}, INFINITY});
 	return fs;
 }
 

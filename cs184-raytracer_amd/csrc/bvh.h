@@ -14,7 +14,6 @@ struct FlatScene {
 	std::vector<DMaterial> materials;
 	std::vector<DLight> lights;
 	std::vector<DFaceGeo> face_geo;
-	std::vector<DFaceCone> face_cone;  // face_geo.size() + kLeafFaces - 1 entries (device_types.h)
 	std::vector<DFaceNrm> face_nrm;
 	std::vector<DBvhNode> nodes;
 	// geometry indices in shadow-test order: the occlusion query is an `any` over the

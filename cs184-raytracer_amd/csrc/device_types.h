@@ -3,10 +3,9 @@
 // HBM layout (all read-only after rt_scene_create):
 //   DGeom[G]        per-geometry record, insertion order (scene.cpp:147 loop order)
 //   DLight[L]       pre-transformed lights, definition order (scene.cpp:117)
-//   DFaceGeo[F]     per face: p0, va = p1-p0, vb = p2-p0 (object space) and the face's
-//                   index within its mesh in the reference's order (tie-break)     80 B
-//   DFaceCone[F+3]  per face: its vertex normals' cone for the facing pre-test      16 B
-//                   (a separate array: a leaf's cones are one 64-B scalar load)
+//   DFaceGeo[F]     per face: p0, va = p1-p0, vb = p2-p0 (object space), the face's
+//                   index within its mesh in the reference's order (tie-break) and its
+//                   normals' cone for the facing pre-test                          96 B
 //   DFaceNrm[F]     per face: n0, n1, n2 (object space, w == 0 dropped)       80 B
 //   DBvhNode[N]     flattened binary LBVH, fp32 child boxes stored in the parent  64 B
 // BVH meshes store their faces in LBVH leaf order; small meshes (<= kLinearFaces) keep
@@ -73,19 +72,13 @@ constexpr double kFacingRel = 1e-5;
 struct alignas(16) DFaceGeo {
 	double p0[3], va[3], vb[3];
 	int32_t id;           // the face's index in the reference's order within its mesh (tie-break)
+	// Facing pre-test (never part of a result): the vertex normals lie within cone_r of the
+	// fp32 vector cone_c; cone_tau = cone_r + margins, rounded up (+inf: no pre-test)
+	float cone_tau;
+	float cone_c[3];
 	int32_t pad;
 };
-static_assert(sizeof(DFaceGeo) == 80, "face record: 80 B");
-
-// Facing pre-test (never part of a result): the vertex normals lie within cone_r of the
-// fp32 vector c; tau = cone_r + margins, rounded up (+inf: no pre-test).  The array has
-// kLeafFaces - 1 trailing entries (tau = +inf), so the cones of any leaf's first face onwards
-// are one 64-B read.
-struct alignas(16) DFaceCone {
-	float c[3];
-	float tau;
-};
-static_assert(sizeof(DFaceCone) == 16, "cone record: 16 B");
+static_assert(sizeof(DFaceGeo) == 96, "face record: 96 B");
 
 struct alignas(16) DFaceNrm {
 	double n0[3], n1[3], n2[3];

@@ -288,11 +288,6 @@ __device__ __forceinline__ void wt_end(unsigned long long t0, uint32_t tag, int6
 #define WT_END(tag, item) ((void)0)
 #endif
 
-// sphere_surely_misses before the sphere tests (exact; 0: always the reference's arithmetic)
-#ifndef RT_SPHERE_PRETEST
-#define RT_SPHERE_PRETEST 1
-#endif
-
 // A mesh hit (face, barycentric a, b), or a sphere hit (face -1, ray parameter t in a)
 struct FaceHit {
 	int32_t face;
@@ -352,9 +347,9 @@ __device__ __forceinline__ bool facing_rejects(float c0, float c1, float c2, flo
 	// s > tau: front false, rejected unless reverse; s < -tau: front true, rejected if reverse
 	return reverse ? s < -tau : s > tau;
 }
-template <typename CP>
-__device__ __forceinline__ bool face_facing_rejects(CP C, V3 d, bool reverse) {
-	return facing_rejects(C->c[0], C->c[1], C->c[2], C->tau, d, reverse);
+template <typename FP>
+__device__ __forceinline__ bool face_facing_rejects(FP F, V3 d, bool reverse) {
+	return facing_rejects(F->cone_c[0], F->cone_c[1], F->cone_c[2], F->cone_tau, d, reverse);
 }
 // One iteration of the face loop of geometry.cpp:78-124.  Accepts the face when it is
 // strictly closer, or equally close with a smaller reference index: over any visiting
@@ -369,8 +364,8 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 #if RT_DIAG_LANES
 	diag_lanes(kAnyHit ? 12 : 14, true);  // [12]/[14] per-lane face tests (shadow/closest): wave slots, lanes
 #endif
-	if (face_facing_rejects(S.fcone + f, d, reverse)) return false;
 	const DFaceGeo* F = S.fgeo + f;
+	if (face_facing_rejects(F, d, reverse)) return false;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	// id is fetched with the vertices: the compiler would otherwise issue its load where it is
 	// first used (one more memory round trip per candidate face)
@@ -418,9 +413,8 @@ __device__ __forceinline__ bool test_face(const DeviceScene& S, int32_t f, V3 o,
 // bool carried through the traversal loop (an i1 loop value costs exec-mask merges on every
 // iteration).  Divisions of failed lanes may see D = 0 (inf/NaN, discarded).  The range
 // tests keep the reference's form (geometry.cpp:93-106: a NaN a, b or t is not rejected).
-// on: the lanes testing the face, keep: the lanes its facing pre-test keeps (test_leaf_pred).
-// Returns the lanes for which kAnyHit && the face passes within any_limit (their question is
-// answered).
+// on: the lanes testing the face.  Returns the lanes for which kAnyHit && the face passes
+// within any_limit (their question is answered).
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 __device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
 // The lanes where a comparison holds.  A ballot of one comparison is the comparison's own
@@ -438,19 +432,21 @@ __device__ __forceinline__ uint64_t quotient_surely_above_m(double num, double d
 template <bool kAnyHit, typename WS>
 __device__ __forceinline__ uint64_t test_face_pred(const DeviceScene& S, int32_t f, V3 o, V3 d, V3 nd, double dn,
                                                    bool reverse, double any_limit, MeshBest& best, WS& ws,
-                                                   uint64_t on, uint64_t keep) {
+                                                   uint64_t on) {
 	ws.add(W_TRIS, lane_in(on));
 	DIAG_WT(1);
-	uint64_t ok = on & keep;
-	DIAG_PK(kAnyHit ? PK_FACE : PK_C_FACE, lane_in(on));
-	if (!ok) return 0;
-	if (kAnyHit) DIAG_PK(PK_FACE_FACING, lane_in(ok));
-	// the vertices and id in one go (scalar loads, fetched only for faces some lane keeps)
 	const auto F = uniform_ptr(S.fgeo) + f;
 	const V3 p0 = load3(F->p0), va = load3(F->va), vb = load3(F->vb);
 	const int32_t id = F->id;
+	const float c0 = F->cone_c[0], c1 = F->cone_c[1], c2 = F->cone_c[2], tau = F->cone_tau;
 	asm volatile("" ::"s"(p0.x), "s"(p0.y), "s"(p0.z), "s"(va.x), "s"(va.y), "s"(va.z), "s"(vb.x), "s"(vb.y),
-	             "s"(vb.z), "s"(id));
+	             "s"(vb.z), "s"(id), "s"(c0), "s"(c1), "s"(c2), "s"(tau));
+	const float sf = facing_dot(c0, c1, c2, d);
+	const uint64_t rev = BAL(reverse);  // (loop-invariant)
+	uint64_t ok = on & ~((BAL(sf < -tau) & rev) | (BAL(sf > tau) & ~rev));
+	DIAG_PK(kAnyHit ? PK_FACE : PK_C_FACE, lane_in(on));
+	if (!ok) return 0;
+	if (kAnyHit) DIAG_PK(PK_FACE_FACING, lane_in(ok));
 	const V3 rhs = o - p0;
 	const double D = det3(va, vb, nd);
 	const double Da = det3(rhs, vb, nd);
@@ -487,33 +483,6 @@ __device__ __forceinline__ uint64_t test_face_pred(const DeviceScene& S, int32_t
 		best.b = b;
 	}
 	return kAnyHit ? ok & BAL(dist < any_limit) : 0;
-}
-
-// The faces [f0, f0 + n) (n <= kLeafFaces) of an LBVH leaf or of a block of a linearly
-// scanned mesh, in order: their cones are one 64-B scalar load (DFaceCone), so the facing
-// pre-test of the whole block costs one memory round trip and a face no lane keeps costs
-// none (its vertices are never fetched).  want: the lanes testing the block; live / done:
-// the running masks of mesh_hit_packet.
-template <bool kAnyHit, typename WS>
-__device__ __forceinline__ void test_leaf_pred(const DeviceScene& S, int32_t f0, int32_t n, V3 o, V3 d, V3 nd,
-                                               double dn, bool reverse, double any_limit, MeshBest& best, WS& ws,
-                                               uint64_t want, uint64_t& live, uint64_t& done) {
-	const auto C = uniform_ptr(S.fcone) + f0;
-	const uint64_t rev = BAL(reverse);
-	uint64_t keep[kLeafFaces];
-#pragma unroll
-	for (int k = 0; k < kLeafFaces; k++) {
-		const float sf = facing_dot(C[k].c[0], C[k].c[1], C[k].c[2], d), tau = C[k].tau;
-		keep[k] = k < n ? ~((BAL(sf < -tau) & rev) | (BAL(sf > tau) & ~rev)) : 0;
-	}
-#pragma unroll
-	for (int k = 0; k < kLeafFaces; k++) {
-		if (k >= n) break;
-		const uint64_t h = test_face_pred<kAnyHit>(S, f0 + k, o, d, nd, dn, reverse, any_limit, best, ws, want & live,
-		                                           keep[k]);
-		done |= h;
-		live &= ~h;
-	}
 }
 
 // Slab test of a padded box; conservative: the interval is widened by a relative 1e-9.
@@ -777,34 +746,6 @@ __device__ __forceinline__ bool sphere_hit(GP G, V3 o, V3 d, bool reverse, doubl
 	return t >= 0;
 }
 
-// Exact pre-test of sphere_hit: true when sphere_hit(G, oo, dd, reverse)
-// with dd = normalized3(draw) certainly returns false, decided from the unnormalised
-// object-space direction `draw` (no square root, no division).  With A = |draw|^2,
-// B = 2 draw.oc, C = |oc|^2 - rr the quadratic's roots are the reference's times |draw|, and
-// its discriminant D = B^2 - 4AC is |draw|^2 times the reference's; both are computed to
-// within ~16 eps of scale = B^2 + 4A(|oc|^2 + |rr|) (scaled by 1 / |draw|^2 for the reference).
-// Certainly no hit when
-//   D < -1e-10 scale                         (the reference's disc < 0), or
-//   !reverse and B > 1e-10 sqrt(scale)       (b > 0: -b - sqrt(disc) < 0, t < 0), or
-//   reverse, B > 1e-10 sqrt(scale) and 4AC > 1e-9 scale
-//                                            (disc < b^2 (1 - 1e-9): -b + sqrt(disc) < 0);
-// the margins exceed the rounding by 10^4 or more.  Magnitudes are kept where no quotient
-// can underflow to -0 (t >= 0 would then hold): scale in [1e-200, 1e200], A in
-// [1e-100, 1e100].  NaN or infinite values fail every test (the reference's arithmetic then
-// decides).  Most sphere tests that pass the world cull are the ray's own sphere seen from
-// its surface outwards (a clearly negative root: the ray starts on it) or near misses, so
-// most lanes skip the normalisation and the quotient.
-template <typename GP>
-__device__ __forceinline__ bool sphere_surely_misses(GP G, V3 oo, V3 draw, bool reverse) {
-	const V3 oc = oo - load3(G->center);
-	const double A = sq4(draw), B = 2 * dot4z(draw, oc), oc2 = sq4(oc), C = oc2 - G->rr;
-	const double D = B * B - (4 * A) * C;
-	const double scale = B * B + (4 * A) * (oc2 + fabs(G->rr));
-	const bool ranged = scale >= 1e-200 && scale <= 1e200 && A >= 1e-100 && A <= 1e100;
-	const bool b_pos = B > 1e-10 * sqrt(scale);
-	return ranged && (D < -1e-10 * scale || (b_pos && (!reverse || (4 * A) * C > 1e-9 * scale)));
-}
-
 // Object-space hit point of a mesh face (face.points_[0] + vec4dFrom3d(a * va + b * vb),
 // geometry.cpp:121) or of a sphere (o + t d, t held in h.a)
 __device__ __forceinline__ V3 face_point(const DeviceScene& S, const FaceHit& h) {
@@ -876,10 +817,7 @@ __device__ bool closest_hit(const DeviceScene& S, V3 o, V3 d, bool reverse, doub
 		// Geometry::calculateIntersectionNormal (geometry.cpp:31-45): object-space ray
 		PROF_BEGIN(tx);
 		const V3 oo = xf_point(G->inv, o);
-		const V3 draw = xf_dir(G->inv, d);
-		// a zero draw fails the pre-test, so ray_dir still raises for it
-		if (RT_SPHERE_PRETEST && (!kMesh || G->kind == DGEOM_SPHERE) && sphere_surely_misses(G, oo, draw, reverse)) continue;
-		const V3 dd = ray_dir(draw, ctr);
+		const V3 dd = ray_dir(xf_dir(G->inv, d), ctr);
 		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
 		bool hit, settled;
@@ -923,8 +861,6 @@ __device__ bool geom_occludes(const DeviceScene& S, GP G, V3 o, V3 d, bool rever
 	const V3 oo = xf_point(G->inv, o);
 	const V3 draw = xf_dir(G->inv, d);
 	if (is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
-	if (RT_SPHERE_PRETEST && (!kMesh || G->kind == DGEOM_SPHERE) && sphere_surely_misses(G, oo, draw, reverse))
-		return false;
 	double nrm;  // object-space length of the unit world direction
 	const V3 dd = normalized3(draw, &nrm);
 	PROF_END(ws, PH_XFORM, tx);
@@ -1014,10 +950,11 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 	if (live) {
 		if (kMesh < kMeshBvh || G->bvh_root < 0) {
 			PROF_BEGIN(tf);
-			const int32_t fe = G->face_begin + G->face_count;
-			for (int32_t f = G->face_begin; f < fe; f += kLeafFaces)
-				test_leaf_pred<kAnyHit>(S, f, min(kLeafFaces, fe - f), o, d, nd, dn, reverse, any_limit, best, ws, live,
-				                        live, done);
+			for (int32_t f = G->face_begin; f < G->face_begin + G->face_count; f++) {
+				const uint64_t h = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws, live);
+				done |= h;
+				live &= ~h;
+			}
 				PROF_END(ws, PH_FACES, tf);
 		} else if (!(RT_DIAG_SKIP & 1)) {
 			ws.add(W_ENTRIES, lane_in(live));
@@ -1087,7 +1024,13 @@ __device__ bool mesh_hit_packet(const DeviceScene& S, GP G, V3 o, V3 d, bool rev
 					if (k == 1 && tested) want &= __ballot((first ? tn0 : tn1) <= lim);
 					if (!want) continue;
 					PROF_BEGIN(tf);
-					test_leaf_pred<kAnyHit>(S, fbase + cf, cc, o, d, nd, dn, reverse, any_limit, best, ws, want, live, done);
+					const int32_t f0 = fbase + cf;
+					for (int32_t f = f0; f < f0 + cc; f++) {
+						const uint64_t h = test_face_pred<kAnyHit>(S, f, o, d, nd, dn, reverse, any_limit, best, ws,
+						                                           want & live);
+						done |= h;
+						live &= ~h;
+					}
 					lim = limit32(fmin(prune_limit(best.dist), prune_cap), r32.s);
 					tested = true;
 					PROF_END(ws, PH_FACES, tf);
@@ -1130,9 +1073,6 @@ __device__ bool closest_hit_packet(const DeviceScene& S, V3 o, V3 d, bool revers
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
-		if (RT_SPHERE_PRETEST && (!kMesh || G->kind == DGEOM_SPHERE) &&
-		    !wave_any(cand && !sphere_surely_misses(G, oo, draw, reverse)))
-			continue;
 		const V3 dd = normalized3(draw);
 		PROF_END(ws, PH_XFORM, tx);
 		FaceHit h{-1, 0, 0};
@@ -1185,9 +1125,6 @@ __device__ bool occluded_packet(const DeviceScene& S, V3 o, V3 d, bool reverse, 
 		const V3 oo = xf_point(G->inv, o);
 		const V3 draw = xf_dir(G->inv, d);
 		if (cand && is_zero3(draw)) raise_error(ctr, DERR_NO_DIRECTION);
-		const bool sphere = !kMesh || G->kind == DGEOM_SPHERE;
-		// lanes that surely miss the sphere drop out; none left: the next geometry
-		if (RT_SPHERE_PRETEST && sphere && !wave_any(cand && !sphere_surely_misses(G, oo, draw, reverse))) continue;
 		double nrm;
 		const V3 dd = normalized3(draw, &nrm);
 		PROF_END(ws, PH_XFORM, tx);

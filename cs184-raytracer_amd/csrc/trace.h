@@ -15,7 +15,6 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	const DMaterial* mats;
 	const DLight* lights;
 	const DFaceGeo* fgeo;
-	const DFaceCone* fcone;
 	const DFaceNrm* fnrm;
 	const DBvhNode* nodes;
 	const int32_t* shadow_order;              // geometry order of the occlusion query
