@@ -1444,6 +1444,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	for (const auto& g : fs.geoms) lbvh = lbvh || (g.kind == rtamd::DGEOM_MESH && g.bvh_root >= 0);
 	if (!lbvh) s->light_major_below_single = s->light_major_below_batch;
 	s->ds.n_geoms = static_cast<int32_t>(fs.geoms.size());
+	s->ds.n_faces = static_cast<int32_t>(fs.face_geo.size());
+	s->ds.n_nodes = static_cast<int32_t>(fs.nodes.size());
 	s->ds.n_may_raise = fs.n_may_raise;
 	bool any_bvh = false;
 	for (const auto& g : fs.geoms) {

@@ -24,6 +24,7 @@ struct DeviceScene {  // device pointers (HBM), immutable after upload
 	int32_t n_geoms, n_lights, n_nonambient;
 	int32_t n_may_raise;                      // geometries with DGeom::may_raise
 	int32_t n_meshes;                         // meshes of the scene
+	int32_t n_faces, n_nodes;                 // records in fgeo, nodes (the L2 warm-up of level 0)
 	int32_t mesh_kind;                        // kernels: 0 spheres only, 1 meshes without LBVHs, 2 with (intersect.h)
 	const int32_t* shadow_light;              // j-th non-ambient light -> light index
 	int32_t work_stats;                       // count the LBVH work (rt_counters node_visits ...); 0 = skip

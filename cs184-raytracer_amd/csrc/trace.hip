@@ -144,6 +144,33 @@ __device__ __forceinline__ int64_t xcd_block() {
 	return base + (b & 7) * g + ((b - base) >> 3);
 }
 
+// L2 warm-up (RT_WARM_L2): the face and node records are fetched by scalar loads, one
+// dependent round trip per node and per face, and a scalar-cache miss is served by the XCD's
+// L2.  At the start of a frame that L2 holds the previous frame's output and ray levels, not
+// the scene, so the first level's long traversals (a row share of C4: one round of waves
+// whose slowest, with 75-120 node iterations, set the launch's length, ~1.4 us per
+// iteration; profiles/round5/wave_times/) wait on the memory behind L2 at every step.  The
+// first blocks of a level-0 launch therefore read the face and node records once per XCD
+// (blocks b = x mod 8 run on XCD x) with coalesced vector loads before their own rays.
+#ifndef RT_WARM_L2
+#define RT_WARM_L2 1
+#endif
+constexpr uint32_t kWarmBlocksPerXcd = 64;
+__device__ __forceinline__ void warm_l2(const DeviceScene& S) {
+	const uint32_t nw = min(gridDim.x / 8, kWarmBlocksPerXcd), slice = blockIdx.x / 8;
+	if (slice >= nw) return;
+	const uint4* fg = reinterpret_cast<const uint4*>(S.fgeo);
+	const uint4* nd = reinterpret_cast<const uint4*>(S.nodes);
+	constexpr int64_t kF = sizeof(DFaceGeo) / 16, kN = sizeof(DBvhNode) / 16;
+	const int64_t nf = int64_t(S.n_faces) * kF, total = nf + int64_t(S.n_nodes) * kN;
+	uint32_t acc = 0;
+	for (int64_t t = int64_t(slice) * blockDim.x + threadIdx.x; t < total; t += int64_t(nw) * blockDim.x) {
+		const uint4 v = t < nf ? fg[t] : nd[t - nf];
+		acc ^= v.x;
+	}
+	asm volatile("" ::"v"(acc));  // the loads are the point: keep them
+}
+
 // std::max(x, 0.0)
 __device__ __forceinline__ double max0(double x) { return (x < 0.0) ? 0.0 : x; }
 
@@ -473,6 +500,7 @@ __global__ void __launch_bounds__(kBlock)
 	}
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+	if (RT_WARM_L2 && kMesh == kMeshBvh && level == 0) warm_l2(S);
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
 		WT_BEGIN();
 		closest_item<kPacket, kCount, kMesh>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
@@ -575,6 +603,7 @@ __global__ void __launch_bounds__(kBlock)
 	}
 	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+	if (RT_WARM_L2 && kMesh == kMeshBvh && level == 0) warm_l2(S);
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
 		WT_BEGIN();
 		closest_item<kPacket, false, kMesh, true>(S, fg, level, n, remaining, plan_last, levels, ctr, stats,
