@@ -222,6 +222,9 @@ struct rt_scene {
 	hipStream_t stream = nullptr;                // default caller stream (rt_render, normalize)
 	rtamd::DeviceScene ds{};
 	std::vector<void*> allocs;
+	// the scene's uploaded block and the bytes staged for it (rt_debug_scene_verify)
+	const void* upload_block = nullptr;
+	std::vector<unsigned char> upload_host;
 	rt_scene_info info{};
 	std::vector<std::unique_ptr<Lane>> lanes;
 	rtamd::DeviceCounters* ctr = nullptr;        // device
@@ -343,9 +346,14 @@ struct UploadBatch {
 		HIP_TRY(hipMalloc(&block, total));
 		s->allocs.push_back(block);
 		void* stage = nullptr;
-		HIP_TRY(hipHostMalloc(&stage, total, hipHostMallocMapped));
+		// coherent (fine-grained): the copy kernel's reads must not hit lines the XCDs' L2s
+		// still hold from an earlier staging buffer at the same addresses (hipHostMalloc's
+		// default memory is non-coherent: GPU accesses are cached in L2).  A recycled stage read
+		// stale corrupted a scene in 3 of 3000 fuzz scenes rendered by 8 processes at once.
+		HIP_TRY(hipHostMalloc(&stage, total, hipHostMallocMapped | hipHostMallocCoherent));
 		void* stage_dev = nullptr;
 		hipError_t e = hipHostGetDevicePointer(&stage_dev, stage, 0);
+		std::memset(stage, 0, total);  // the padding between arrays too (rt_debug_scene_verify)
 		for (const Item& it : items) std::memcpy(static_cast<char*>(stage) + it.offset, it.host, it.bytes);
 		if (e == hipSuccess) e = rtamd::launch_copy16(block, stage_dev, static_cast<int64_t>(total / 16), s->stream);
 		if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
@@ -355,6 +363,9 @@ struct UploadBatch {
 			it.set(static_cast<const char*>(block) + it.offset);
 			s->info.device_bytes += static_cast<int64_t>(it.bytes);
 		}
+		s->upload_block = block;
+		s->upload_host.assign(total, 0);
+		for (const Item& it : items) std::memcpy(s->upload_host.data() + it.offset, it.host, it.bytes);
 		return RT_OK;
 	}
 };
@@ -365,6 +376,18 @@ struct UploadBatch {
 // need once the call is done (right_size_levels), and are kept for later renders.
 // bytes of one level buffer of `n` ray slots: 21 double arrays, 4 int32 arrays, two flag
 // arrays, n x lights shadow verdicts and the level's counts, each 256-B aligned
+// Clears device memory and waits for it.  hipMemset is asynchronous for device memory and
+// runs on the null stream, which the library's non-blocking streams do not wait for: a
+// kernel queued on a lane's stream right after it could run first.  Under a GPU shared by
+// several processes that happened (a level's counts cleared after its k_closest had started
+// appending: lost hits, black pixels, 0.2% of the production-schedule fuzz scenes rendered by
+// 8 processes at once; rounds 1-5).
+hipError_t clear_device(void* p, size_t bytes) {
+	hipError_t e = hipMemsetAsync(p, 0, bytes, nullptr);
+	if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+	return e;
+}
+
 int64_t level_block_bytes(const rt_scene* s, int64_t n) {
 	const int64_t nl = std::max(1, s->ds.n_nonambient);
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
@@ -412,7 +435,7 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	L.lv.hinside = reinterpret_cast<uint8_t*>(take(n));
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
-	HIP_TRY(hipMemset(L.lv.counts, 0, 4 * sizeof(int32_t)));
+	HIP_TRY(clear_device(L.lv.counts, 4 * sizeof(int32_t)));
 	L.lv.capacity = capacity;
 	return RT_OK;
 }
@@ -433,9 +456,9 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		const size_t cap = std::max<size_t>(16, 2 * (level + 1));
 		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
 		int32_t* counts = nullptr;
-		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), hipHostMallocCoherent));
 		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dev), cap * sizeof(rtamd::RayLevel)));
-		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&counts), 2 * cap * sizeof(int32_t), hipHostMallocDefault));
+		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&counts), 2 * cap * sizeof(int32_t), hipHostMallocCoherent));
 		std::memset(pin, 0, cap * sizeof(rtamd::RayLevel));
 		if (ln.levels_pinned) {
 			std::memcpy(pin, ln.levels_pinned, ln.levels_cap * sizeof(rtamd::RayLevel));
@@ -445,7 +468,11 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 			(void)hipFree(ln.levels_dev);
 		}
 		ln.counts_host = counts;
-		HIP_TRY(hipMemcpy(dev, pin, cap * sizeof(rtamd::RayLevel), hipMemcpyHostToDevice));
+		// on the lane's stream, ahead of the per-level record updates queued there: a hipMemcpy
+		// (the null stream, another hardware queue) could land after such an update and put a
+		// zeroed record back (kernels then write through null level pointers: black rows, 0.2% of
+		// the fuzz scenes when 8 processes shared the GPU; rounds 1-5)
+		HIP_TRY(hipMemcpyAsync(dev, pin, cap * sizeof(rtamd::RayLevel), hipMemcpyHostToDevice, ln.stream));
 		ln.levels_pinned = pin;
 		ln.levels_dev = dev;
 		ln.levels_cap = cap;
@@ -905,7 +932,7 @@ struct Render {
 			const int64_t cap = std::max<int64_t>(n_rows, 1024);
 			HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ln.rows_dev), cap * sizeof(rtamd::ChunkRow)));
 			HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.rows_pin), cap * sizeof(rtamd::ChunkRow),
-			                      hipHostMallocDefault));
+			                      hipHostMallocCoherent));
 			ln.rows_cap = cap;
 		}
 		uint64_t h = 1469598103934665603ull;
@@ -1470,13 +1497,14 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	HIP_TRY(hipMalloc(&fd, kFinDoneBytes));
 	s->allocs.push_back(fd);
 	s->fin_done = static_cast<uint32_t*>(fd);
-	HIP_TRY(hipMemset(s->fin_done, 0, kFinDoneBytes));
+	HIP_TRY(clear_device(s->fin_done, kFinDoneBytes));
 	void* sm = nullptr;
 	HIP_TRY(hipMalloc(&sm, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1)));
 	s->allocs.push_back(sm);
 	s->summary = static_cast<unsigned long long*>(sm);
+	// written by the kernels, read by the host: coherent, so no L2 line of it outlives a call
 	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->summary_host), sizeof(unsigned long long) * (rtamd::ST_COUNT + 1),
-	                      hipHostMallocDefault));
+	                      hipHostMallocMapped | hipHostMallocCoherent));
 	{
 		void* mapped = nullptr;
 		if (hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
@@ -1484,8 +1512,8 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 		(void)hipGetLastError();
 	}
 	// statistics and the error word start cleared; k_stats_finish clears them after each render
-	HIP_TRY(hipMemset(s->ctr, 0, sizeof(rtamd::DeviceCounters)));
-	HIP_TRY(hipMemset(s->stats, 0, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
+	HIP_TRY(clear_device(s->ctr, sizeof(rtamd::DeviceCounters)));
+	HIP_TRY(clear_device(s->stats, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
 	rt_scene_info& in = s->info;
 	in.n_geometries = s->ds.n_geoms;
 	for (const auto& g : fs.geoms) (g.kind == rtamd::GEOM_SPHERE ? in.n_spheres : in.n_meshes)++;
@@ -2015,13 +2043,18 @@ hipError_t copy_to_host(void* dst, const void* src, size_t bytes) {
 // mapped pinned host staging the kernels write the image into, for images of
 // at most kMappedStageMax bytes (f64 + RGB8: a 2560x1600 frame; a 4096^2 f64 image, 400 MB,
 // is copied instead of pinning that much host memory for the scene's lifetime)
-constexpr size_t kMappedStageMax = size_t(128) << 20;
+#ifndef RT_MAPPED_STAGE_MAX
+#define RT_MAPPED_STAGE_MAX (size_t(128) << 20)
+#endif
+constexpr size_t kMappedStageMax = RT_MAPPED_STAGE_MAX;
 int ensure_mapped_stage(rt_scene* s, size_t bytes) {
 	if (s->mapped_stage_bytes >= bytes) return RT_OK;
 	if (s->mapped_stage) (void)hipHostFree(s->mapped_stage);
 	s->mapped_stage = s->mapped_stage_dev = nullptr;
 	s->mapped_stage_bytes = 0;
-	if (hipHostMalloc(&s->mapped_stage, std::max<size_t>(bytes, 256), hipHostMallocMapped) != hipSuccess) {
+	// coherent: the kernels' image writes reach host memory, not an L2 line (see UploadBatch)
+	if (hipHostMalloc(&s->mapped_stage, std::max<size_t>(bytes, 256), hipHostMallocMapped | hipHostMallocCoherent) !=
+	    hipSuccess) {
 		s->mapped_stage = nullptr;
 		return fail(RT_ERR_DEVICE, "hipHostMalloc (mapped image stage) failed");
 	}
@@ -2224,6 +2257,69 @@ int rt_debug_wave_times(int device, void* out, int max_records) {
 	const int n = rtamd::read_wave_times(out, max_records);
 	if (n < 0) return fail(RT_ERR_DEVICE, "wave time read-back failed");
 	return n;
+}
+
+// Diagnostic: the scene's device block read back and compared with the bytes staged for it:
+// the number of differing 16-B words (0: intact).
+// Not in rtamd.h.
+int rt_debug_scene_verify(rt_scene* s) {
+	if (!s) return fail(RT_ERR_ARG, "null scene");
+	if (!s->upload_block) return 0;
+	HIP_TRY(hipSetDevice(s->device));
+	HIP_TRY(hipDeviceSynchronize());
+	std::vector<unsigned char> back(s->upload_host.size());
+	HIP_TRY(hipMemcpy(back.data(), s->upload_block, back.size(), hipMemcpyDeviceToHost));
+	int bad = 0;
+	for (size_t w = 0; w + 16 <= back.size(); w += 16)
+		bad += std::memcmp(back.data() + w, s->upload_host.data() + w, 16) != 0;
+	return bad;
+}
+
+// Diagnostic: the last host-image render's f64 image read again from where the kernels wrote
+// it (the mapped stage, else the device staging image), after a device synchronisation.
+// Not in rtamd.h.
+int rt_debug_read_stage(rt_scene* s, double* out, int64_t n_values) {
+	if (!s || !out) return fail(RT_ERR_ARG, "null scene or output");
+	HIP_TRY(hipSetDevice(s->device));
+	HIP_TRY(hipDeviceSynchronize());
+	const size_t bytes = static_cast<size_t>(n_values) * sizeof(double);
+	if (s->mapped_stage && s->mapped_stage_bytes >= bytes) {
+		std::memcpy(out, s->mapped_stage, bytes);
+		return 1;
+	}
+	if (s->out_dev) {
+		HIP_TRY(hipMemcpy(out, s->out_dev, bytes, hipMemcpyDeviceToHost));
+		return 2;
+	}
+	return 0;
+}
+
+// Diagnostic: every lane's cached row tables read back and compared with their host copies:
+// the number of rows that differ.  Not in rtamd.h.
+int rt_debug_rows_verify(rt_scene* s) {
+	if (!s) return fail(RT_ERR_ARG, "null scene");
+	HIP_TRY(hipSetDevice(s->device));
+	HIP_TRY(hipDeviceSynchronize());
+	int bad = 0;
+	for (auto& lp : s->lanes)
+		for (const auto& t : lp->tables) {
+			if (!t.dev || t.host.empty()) continue;
+			std::vector<rtamd::ChunkRow> back(t.host.size());
+			HIP_TRY(hipMemcpy(back.data(), t.dev, back.size() * sizeof(rtamd::ChunkRow), hipMemcpyDeviceToHost));
+			for (size_t k = 0; k < back.size(); k++)
+				bad += std::memcmp(&back[k], &t.host[k], sizeof(rtamd::ChunkRow)) != 0;
+		}
+	return bad;
+}
+
+// Diagnostic: a system-scope cache invalidation on every XCD (L2 and L1 non-coherent lines
+// dropped), synchronised.  Not in rtamd.h.
+int rt_debug_invalidate_caches(int device) {
+	HIP_TRY(hipSetDevice(device));
+	HIP_TRY(hipDeviceSynchronize());
+	HIP_TRY(rtamd::launch_invalidate_caches(nullptr));
+	HIP_TRY(hipDeviceSynchronize());
+	return RT_OK;
 }
 
 int rt_selftest_math(int device, int op, const double* x, const double* y, double* out, int64_t n) {

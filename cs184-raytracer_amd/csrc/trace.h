@@ -199,6 +199,8 @@ hipError_t read_phase_profile(unsigned long long* out /* 4 * kPhaseSlots */);
 // RT_DIAG_WAVETIME builds: the wave records since the last call (32 B each, intersect.h
 // WaveTime), at most max_records, then cleared; 0 in other builds, -1 on a HIP error
 int read_wave_times(void* out, int max_records);
+// every XCD's L2 and the CUs' L1s drop their non-coherent lines (system-scope acquire)
+hipError_t launch_invalidate_caches(hipStream_t stream);
 // FETCH_SIZE calibration: reads `bytes` of buf once, `width` (1, 4, 8, 16) bytes per lane
 // VALU issue calibration: kind 0 v_fma_f32, 1 v_pk_fma_f32, 2 v_fma_f64 chains at
 // waves_per_simd waves on every SIMD

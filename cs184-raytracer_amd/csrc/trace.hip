@@ -1334,6 +1334,17 @@ hipError_t read_phase_profile(unsigned long long* out) {
 #endif
 }
 
+// A system-scope acquire on every XCD (buffer_inv sc0 sc1: the CU's L1 and its XCD's L2 drop
+// their non-coherent lines): 2048 blocks, dealt round-robin over the XCDs and their CUs
+__global__ void k_invalidate_caches() {
+	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+hipError_t launch_invalidate_caches(hipStream_t stream) {
+	hipLaunchKernelGGL(k_invalidate_caches, dim3(2048), dim3(64), 0, stream);  // every CU, every XCD
+	return hipGetLastError();
+}
+
 int read_wave_times(void* out, int max_records) {
 #if RT_DIAG_WAVETIME
 	unsigned int n = 0;

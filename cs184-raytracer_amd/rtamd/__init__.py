@@ -181,7 +181,11 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    # the ctypes structs above mirror include/rtamd.h of this ABI version
+    # the ctypes structs above mirror include/rtamd.h of this ABI version (RTAMD_ABI_CHECK=0
+    # loads a library of an older revision for a bisection: its structs must be a prefix of these)
+    if os.environ.get("RTAMD_ABI_CHECK") == "0" and not hasattr(L, "rt_abi_version"):
+        _lib = L
+        return L
     L.rt_abi_version.restype, L.rt_abi_version.argtypes = i32, []
     if L.rt_abi_version() != RTAMD_ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has ABI version {L.rt_abi_version()}, this binding expects "

@@ -9,6 +9,7 @@ The image (binary64 bit patterns, NaN payloads and -0 included) and the referenc
 counters must equal the oracle's (pinned to the unmodified reference, test_oracle.py).
 The generator is seeded: a failing seed reproduces exactly.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -127,10 +128,11 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
         again = s.renderScene(options=opts)
         assert np.array_equal(np.ascontiguousarray(again).view(np.uint64), np.ascontiguousarray(got).view(np.uint64))
         assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (st.trace_rays, st.shadow_rays)
-    s.close()
     g, r = np.ascontiguousarray(got).view(np.uint64), np.ascontiguousarray(want).view(np.uint64)
     diff = int((g != r).any(axis=2).sum())
-    assert diff == 0, f"seed {seed}: {diff} pixels differ from the oracle"
+    if diff:
+        raise AssertionError(_diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st))
+    s.close()
     assert (st.trace_rays, st.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
 
 
@@ -161,3 +163,50 @@ def test_random_scene_batch_partition(gpu, oracle, tmp_path, seed):
         ref = np.ascontiguousarray(want[r]).view(np.uint64)
         assert int((g != ref).any(axis=2).sum()) == 0, f"seed {seed}"
     s.close()
+
+
+def _rays(st):
+    return [st.trace_rays, st.shadow_rays, st.reflect_rays, st.refract_rays]
+
+
+def _ndiff(x, y):
+    return int((np.ascontiguousarray(x).view(np.uint64) != np.ascontiguousarray(y).view(np.uint64)).any(axis=2).sum())
+
+
+def _diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st):
+    """Which side moved on a mismatch: the last image read again where the kernels wrote it, the
+    scene's device block and row table against their host copies, a render after every XCD's caches
+    dropped their lines, the oracle again on one thread, and a scene rendered from scratch."""
+    L = gpu.lib()
+    for name, args in (("rt_debug_read_stage", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
+                       ("rt_debug_scene_verify", [ctypes.c_void_p]), ("rt_debug_rows_verify", [ctypes.c_void_p]),
+                       ("rt_debug_invalidate_caches", [ctypes.c_int])):
+        getattr(L, name).argtypes = args
+    buf = np.empty_like(got)
+    where = L.rt_debug_read_stage(s.handle, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+    reread = (where, _ndiff(buf, want))
+    bad_words, bad_rows = L.rt_debug_scene_verify(s.handle), L.rt_debug_rows_verify(s.handle)
+    L.rt_debug_invalidate_caches(0)
+    after_inv = _ndiff(s.renderScene(options=opts), want)
+    st_inv = s.last_stats
+    s.close()
+    want1, _ = oracle.render(path, opts.renderWidth_, opts.renderHeight_, bdepth=opts.bounceDepth_,
+                             intersection_only=opts.intersectionOnly_, threads=1)
+    s = gpu.load_scene(path)
+    fresh = s.renderScene(options=opts)
+    st_fresh = s.last_stats
+    s.close()
+    dump = os.environ.get("RTAMD_FUZZ_DUMP")  # a directory for the images of a failing seed
+    if dump:
+        os.makedirs(dump, exist_ok=True)
+        np.savez(os.path.join(dump, f"seed{seed}.npz"), got=got, want=want, fresh=fresh)
+    ys, xs = np.nonzero((np.ascontiguousarray(got).view(np.uint64)
+                         != np.ascontiguousarray(want).view(np.uint64)).any(axis=2))
+    return (f"seed {seed}: {len(ys)} pixels differ from the oracle (first {list(zip(ys[:4].tolist(), xs[:4].tolist()))}); "
+            f"oracle on 1 thread vs the first oracle: {_ndiff(want1, want)}; fresh scene vs oracle: "
+            f"{_ndiff(fresh, want)}, vs the first render: {_ndiff(fresh, got)}; after a cache invalidation vs "
+            f"oracle: {after_inv}; scene block words differing from the upload: {bad_words}; row-table entries "
+            f"differing: {bad_rows}; last image read again (where, differing pixels): {reread}; rays "
+            f"(trace, shadow, reflect, refract): oracle "
+            f"{[cnt[k] for k in ('trace_rays', 'shadow_rays', 'reflect_rays', 'refract_rays')]}, first {_rays(st)}, "
+            f"after invalidation {_rays(st_inv)}, fresh {_rays(st_fresh)}")
