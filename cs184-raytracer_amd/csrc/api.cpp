@@ -378,10 +378,7 @@ struct UploadBatch {
 // arrays, n x lights shadow verdicts and the level's counts, each 256-B aligned
 // Clears device memory and waits for it.  hipMemset is asynchronous for device memory and
 // runs on the null stream, which the library's non-blocking streams do not wait for: a
-// kernel queued on a lane's stream right after it could run first.  Under a GPU shared by
-// several processes that happened (a level's counts cleared after its k_closest had started
-// appending: lost hits, black pixels, 0.2% of the production-schedule fuzz scenes rendered by
-// 8 processes at once; rounds 1-5).
+// kernel queued on a lane's stream right after it could otherwise run first.
 hipError_t clear_device(void* p, size_t bytes) {
 	hipError_t e = hipMemsetAsync(p, 0, bytes, nullptr);
 	if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
@@ -470,8 +467,7 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		ln.counts_host = counts;
 		// on the lane's stream, ahead of the per-level record updates queued there: a hipMemcpy
 		// (the null stream, another hardware queue) could land after such an update and put a
-		// zeroed record back (kernels then write through null level pointers: black rows, 0.2% of
-		// the fuzz scenes when 8 processes shared the GPU; rounds 1-5)
+		// zeroed record back
 		HIP_TRY(hipMemcpyAsync(dev, pin, cap * sizeof(rtamd::RayLevel), hipMemcpyHostToDevice, ln.stream));
 		ln.levels_pinned = pin;
 		ln.levels_dev = dev;

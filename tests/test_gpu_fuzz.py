@@ -102,6 +102,16 @@ _SEEDS = int(os.environ.get("RTAMD_FUZZ_SEEDS", "256"))
 _W, _H = (int(v) for v in os.environ.get("RTAMD_FUZZ_SIZE", "56x40").split("x"))  # image size of the sweep
 
 
+_KEPT = []  # RTAMD_FUZZ_KEEP=1: the scenes stay open to the end of the process (no device memory freed)
+
+
+def _close(s):
+    if os.environ.get("RTAMD_FUZZ_KEEP") == "1":
+        _KEPT.append(s)
+    else:
+        s.close()
+
+
 @pytest.mark.parametrize("seed", range(_BASE, _BASE + _SEEDS))
 def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
     # odd seeds: the production light-major threshold (every launch here is below it);
@@ -132,7 +142,7 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
     diff = int((g != r).any(axis=2).sum())
     if diff:
         raise AssertionError(_diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st))
-    s.close()
+    _close(s)
     assert (st.trace_rays, st.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
 
 
