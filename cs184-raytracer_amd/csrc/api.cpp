@@ -320,6 +320,16 @@ struct rt_scene {
 
 namespace {
 
+// Pinned host memory (staging, records, counts, the summary and the mapped image stage):
+// fine-grained (coherent) by default, so that no GPU cache holds a line of it between a
+// kernel's write and the host's read; RT_PINNED_COHERENT=0 builds round 4's coarse-grained
+// allocations (A/B of the cost on the mapped image writes).
+#ifndef RT_PINNED_COHERENT
+#define RT_PINNED_COHERENT 1
+#endif
+constexpr unsigned kPinned = RT_PINNED_COHERENT ? hipHostMallocCoherent : hipHostMallocDefault;
+constexpr unsigned kPinnedMapped = hipHostMallocMapped | (RT_PINNED_COHERENT ? hipHostMallocCoherent : 0u);
+
 // The scene's arrays in one device block, filled in one launch from mapped pinned staging
 // (RTAMD_UPLOAD 1): one allocation, no copy engine (its first use in a process costs ~16 ms
 // and every pageable hipMemcpy ~3 ms; profiles/round4 CLI traces).  add() records where each
@@ -350,7 +360,7 @@ struct UploadBatch {
 		// still hold from an earlier staging buffer at the same addresses (hipHostMalloc's
 		// default memory is non-coherent: GPU accesses are cached in L2).  A recycled stage read
 		// stale corrupted a scene in 3 of 3000 fuzz scenes rendered by 8 processes at once.
-		HIP_TRY(hipHostMalloc(&stage, total, hipHostMallocMapped | hipHostMallocCoherent));
+		HIP_TRY(hipHostMalloc(&stage, total, kPinnedMapped));
 		void* stage_dev = nullptr;
 		hipError_t e = hipHostGetDevicePointer(&stage_dev, stage, 0);
 		std::memset(stage, 0, total);  // the padding between arrays too (rt_debug_scene_verify)
@@ -453,9 +463,9 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		const size_t cap = std::max<size_t>(16, 2 * (level + 1));
 		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
 		int32_t* counts = nullptr;
-		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), hipHostMallocCoherent));
+		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), kPinned));
 		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dev), cap * sizeof(rtamd::RayLevel)));
-		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&counts), 2 * cap * sizeof(int32_t), hipHostMallocCoherent));
+		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&counts), 2 * cap * sizeof(int32_t), kPinned));
 		std::memset(pin, 0, cap * sizeof(rtamd::RayLevel));
 		if (ln.levels_pinned) {
 			std::memcpy(pin, ln.levels_pinned, ln.levels_cap * sizeof(rtamd::RayLevel));
@@ -928,7 +938,7 @@ struct Render {
 			const int64_t cap = std::max<int64_t>(n_rows, 1024);
 			HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ln.rows_dev), cap * sizeof(rtamd::ChunkRow)));
 			HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.rows_pin), cap * sizeof(rtamd::ChunkRow),
-			                      hipHostMallocCoherent));
+			                      kPinned));
 			ln.rows_cap = cap;
 		}
 		uint64_t h = 1469598103934665603ull;
@@ -1498,9 +1508,9 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	HIP_TRY(hipMalloc(&sm, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1)));
 	s->allocs.push_back(sm);
 	s->summary = static_cast<unsigned long long*>(sm);
-	// written by the kernels, read by the host: coherent, so no L2 line of it outlives a call
+	// written by the kernels, read by the host
 	HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&s->summary_host), sizeof(unsigned long long) * (rtamd::ST_COUNT + 1),
-	                      hipHostMallocMapped | hipHostMallocCoherent));
+	                      kPinned));
 	{
 		void* mapped = nullptr;
 		if (hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
@@ -2049,7 +2059,7 @@ int ensure_mapped_stage(rt_scene* s, size_t bytes) {
 	s->mapped_stage = s->mapped_stage_dev = nullptr;
 	s->mapped_stage_bytes = 0;
 	// coherent: the kernels' image writes reach host memory, not an L2 line (see UploadBatch)
-	if (hipHostMalloc(&s->mapped_stage, std::max<size_t>(bytes, 256), hipHostMallocMapped | hipHostMallocCoherent) !=
+	if (hipHostMalloc(&s->mapped_stage, std::max<size_t>(bytes, 256), kPinnedMapped) !=
 	    hipSuccess) {
 		s->mapped_stage = nullptr;
 		return fail(RT_ERR_DEVICE, "hipHostMalloc (mapped image stage) failed");
