@@ -2318,6 +2318,31 @@ int rt_debug_rows_verify(rt_scene* s) {
 	return bad;
 }
 
+// Diagnostic: every lane's device level records and row table against their pinned
+// sources; the number of differing records/rows.  Not in rtamd.h.
+int rt_debug_levels_verify(rt_scene* s) {
+	if (!s) return fail(RT_ERR_ARG, "null scene");
+	HIP_TRY(hipSetDevice(s->device));
+	HIP_TRY(hipDeviceSynchronize());
+	int bad = 0;
+	for (auto& lp : s->lanes) {
+		const Lane& ln = *lp;
+		if (ln.levels_dev && ln.levels_cap) {
+			std::vector<rtamd::RayLevel> back(ln.levels_cap);
+			HIP_TRY(hipMemcpy(back.data(), ln.levels_dev, back.size() * sizeof(rtamd::RayLevel), hipMemcpyDeviceToHost));
+			for (size_t k = 0; k < back.size(); k++)
+				bad += std::memcmp(&back[k], &ln.levels_pinned[k], sizeof(rtamd::RayLevel)) != 0;
+		}
+		if (ln.rows_dev && ln.rows_pin && ln.rows_uploaded > 0) {
+			std::vector<rtamd::ChunkRow> back(static_cast<size_t>(ln.rows_uploaded));
+			HIP_TRY(hipMemcpy(back.data(), ln.rows_dev, back.size() * sizeof(rtamd::ChunkRow), hipMemcpyDeviceToHost));
+			for (size_t k = 0; k < back.size(); k++)
+				bad += 1000 * (std::memcmp(&back[k], &ln.rows_pin[k], sizeof(rtamd::ChunkRow)) != 0);
+		}
+	}
+	return bad;
+}
+
 // Diagnostic: a system-scope cache invalidation on every XCD (L2 and L1 non-coherent lines
 // dropped), synchronised.  Not in rtamd.h.
 int rt_debug_invalidate_caches(int device) {

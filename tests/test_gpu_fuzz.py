@@ -190,12 +190,14 @@ def _diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st):
     L = gpu.lib()
     for name, args in (("rt_debug_read_stage", [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]),
                        ("rt_debug_scene_verify", [ctypes.c_void_p]), ("rt_debug_rows_verify", [ctypes.c_void_p]),
+                       ("rt_debug_levels_verify", [ctypes.c_void_p]),
                        ("rt_debug_invalidate_caches", [ctypes.c_int])):
         getattr(L, name).argtypes = args
     buf = np.empty_like(got)
     where = L.rt_debug_read_stage(s.handle, buf.ctypes.data_as(ctypes.c_void_p), buf.size)
     reread = (where, _ndiff(buf, want))
     bad_words, bad_rows = L.rt_debug_scene_verify(s.handle), L.rt_debug_rows_verify(s.handle)
+    bad_levels = L.rt_debug_levels_verify(s.handle)
     L.rt_debug_invalidate_caches(0)
     after_inv = _ndiff(s.renderScene(options=opts), want)
     st_inv = s.last_stats
@@ -216,7 +218,7 @@ def _diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st):
             f"oracle on 1 thread vs the first oracle: {_ndiff(want1, want)}; fresh scene vs oracle: "
             f"{_ndiff(fresh, want)}, vs the first render: {_ndiff(fresh, got)}; after a cache invalidation vs "
             f"oracle: {after_inv}; scene block words differing from the upload: {bad_words}; row-table entries "
-            f"differing: {bad_rows}; last image read again (where, differing pixels): {reread}; rays "
+            f"differing: {bad_rows}; level records differing (+1000 per chunk row): {bad_levels}; last image read again (where, differing pixels): {reread}; rays "
             f"(trace, shadow, reflect, refract): oracle "
             f"{[cnt[k] for k in ('trace_rays', 'shadow_rays', 'reflect_rays', 'refract_rays')]}, first {_rays(st)}, "
             f"after invalidation {_rays(st_inv)}, fresh {_rays(st_fresh)}")
