@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 #include "../../include/rtamd.h"
@@ -330,6 +331,50 @@ namespace {
 constexpr unsigned kPinned = RT_PINNED_COHERENT ? hipHostMallocCoherent : hipHostMallocDefault;
 constexpr unsigned kPinnedMapped = hipHostMallocMapped | (RT_PINNED_COHERENT ? hipHostMallocCoherent : 0u);
 
+// Device allocations.  RT_GUARD_BYTES > 0 (a diagnostic build, tools/build_variant.sh)
+// follows every allocation, and every array of a level block, with that many bytes of a
+// known pattern; rt_debug_guards_check counts the guards a kernel has written into (an
+// out-of-bounds write of the library's own).
+#ifndef RT_GUARD_BYTES
+#define RT_GUARD_BYTES 0
+#endif
+constexpr size_t kGuard = RT_GUARD_BYTES;
+constexpr unsigned char kGuardByte = 0xA5;
+struct GuardRegion {
+	const void* base;  // the allocation it belongs to
+	char* at;
+	size_t bytes;
+	size_t offset;     // from base
+};
+std::mutex g_guard_mu;
+std::vector<GuardRegion>& guard_regions() {
+	static auto* v = new std::vector<GuardRegion>();
+	return *v;
+}
+hipError_t guard_add(const void* base, char* at, size_t bytes) {
+	hipError_t e = hipMemset(at, kGuardByte, bytes);
+	if (e == hipSuccess) e = hipDeviceSynchronize();
+	std::lock_guard<std::mutex> lk(g_guard_mu);
+	guard_regions().push_back({base, at, bytes, static_cast<size_t>(at - static_cast<const char*>(base))});
+	return e;
+}
+template <typename T>
+hipError_t dev_alloc(T** p, size_t bytes) {
+	void* q = nullptr;
+	hipError_t e = hipMalloc(&q, bytes + kGuard);
+	*p = static_cast<T*>(q);
+	if (e == hipSuccess && kGuard) e = guard_add(q, static_cast<char*>(q) + bytes, kGuard);
+	return e;
+}
+hipError_t dev_free(void* p) {
+	if (kGuard && p) {
+		std::lock_guard<std::mutex> lk(g_guard_mu);
+		auto& v = guard_regions();
+		v.erase(std::remove_if(v.begin(), v.end(), [p](const GuardRegion& g) { return g.base == p; }), v.end());
+	}
+	return hipFree(p);
+}
+
 // The scene's arrays in one device block, filled in one launch from mapped pinned staging
 // (RTAMD_UPLOAD 1): one allocation, no copy engine (its first use in a process costs ~16 ms
 // and every pageable hipMemcpy ~3 ms; profiles/round4 CLI traces).  add() records where each
@@ -353,13 +398,11 @@ struct UploadBatch {
 	int commit(rt_scene* s) {
 		if (total == 0) return RT_OK;
 		void* block = nullptr;
-		HIP_TRY(hipMalloc(&block, total));
+		HIP_TRY(dev_alloc(&block, total));
 		s->allocs.push_back(block);
 		void* stage = nullptr;
-		// coherent (fine-grained): the copy kernel's reads must not hit lines the XCDs' L2s
-		// still hold from an earlier staging buffer at the same addresses (hipHostMalloc's
-		// default memory is non-coherent: GPU accesses are cached in L2).  A recycled stage read
-		// stale corrupted a scene in 3 of 3000 fuzz scenes rendered by 8 processes at once.
+		// coherent (fine-grained) by default (kPinnedMapped): the copy kernel's reads cannot hit
+		// lines an XCD's L2 still holds from an earlier staging buffer at the same addresses
 		HIP_TRY(hipHostMalloc(&stage, total, kPinnedMapped));
 		void* stage_dev = nullptr;
 		hipError_t e = hipHostGetDevicePointer(&stage_dev, stage, 0);
@@ -398,7 +441,7 @@ hipError_t clear_device(void* p, size_t bytes) {
 int64_t level_block_bytes(const rt_scene* s, int64_t n) {
 	const int64_t nl = std::max(1, s->ds.n_nonambient);
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	return 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
+	return 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256 + 29 * static_cast<int64_t>(kGuard);
 }
 
 constexpr int kBudgetMiss = 2;  // internal return code: RTAMD_LEVEL_BUDGET exceeded (render_jobs)
@@ -415,19 +458,22 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	if (s->level_budget > 0 && s->info.level_bytes - L.bytes + bytes > s->level_budget) return kBudgetMiss;
 	if (L.block) {
 		HIP_TRY(hipDeviceSynchronize());
-		HIP_TRY(hipFree(L.block));
+		HIP_TRY(dev_free(L.block));
 		L.block = nullptr;
 		s->info.level_bytes -= L.bytes;
 		L.bytes = 0;
 	}
-	HIP_TRY(hipMalloc(&L.block, bytes));
+	HIP_TRY(dev_alloc(&L.block, bytes));
 	L.bytes = bytes;
 	s->info.level_bytes += bytes;
 	s->info.level_bytes_peak = std::max(s->info.level_bytes_peak, s->info.level_bytes);
 	char* p = static_cast<char*>(L.block);
+	std::vector<char*> gaps;  // RT_GUARD_BYTES: the guard after each array
 	auto take = [&](int64_t b) {
 		char* r = p;
 		p += align(b);
+		if (kGuard) gaps.push_back(p);
+		p += static_cast<int64_t>(kGuard);
 		return r;
 	};
 	double** d[21] = {&L.lv.ox, &L.lv.oy, &L.lv.oz, &L.lv.dx,  &L.lv.dy,  &L.lv.dz,  &L.lv.hpx,
@@ -442,6 +488,7 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	L.lv.hinside = reinterpret_cast<uint8_t*>(take(n));
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
+	for (char* g : gaps) HIP_TRY(guard_add(L.block, g, kGuard));
 	HIP_TRY(clear_device(L.lv.counts, 4 * sizeof(int32_t)));
 	L.lv.capacity = capacity;
 	return RT_OK;
@@ -464,7 +511,7 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		rtamd::RayLevel *pin = nullptr, *dev = nullptr;
 		int32_t* counts = nullptr;
 		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&pin), cap * sizeof(rtamd::RayLevel), kPinned));
-		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&dev), cap * sizeof(rtamd::RayLevel)));
+		HIP_TRY(dev_alloc((&dev), cap * sizeof(rtamd::RayLevel)));
 		HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&counts), 2 * cap * sizeof(int32_t), kPinned));
 		std::memset(pin, 0, cap * sizeof(rtamd::RayLevel));
 		if (ln.levels_pinned) {
@@ -472,7 +519,7 @@ int ensure_level_record(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 			std::memcpy(counts, ln.counts_host, 2 * ln.levels_cap * sizeof(int32_t));
 			(void)hipHostFree(ln.levels_pinned);
 			(void)hipHostFree(ln.counts_host);
-			(void)hipFree(ln.levels_dev);
+			(void)dev_free(ln.levels_dev);
 		}
 		ln.counts_host = counts;
 		// on the lane's stream, ahead of the per-level record updates queued there: a hipMemcpy
@@ -530,14 +577,14 @@ int lane_create(Lane& ln, int prio_low, int prio_high) {
 
 void lane_destroy(Lane& ln) {
 	clear_plans(ln);
-	if (ln.rows_dev) (void)hipFree(ln.rows_dev);
+	if (ln.rows_dev) (void)dev_free(ln.rows_dev);
 	if (ln.rows_pin) (void)hipHostFree(ln.rows_pin);
 	for (auto& t : ln.tables)
-		if (t.dev) (void)hipFree(t.dev);
+		if (t.dev) (void)dev_free(t.dev);
 	for (auto& L : ln.levels)
-		if (L.block) (void)hipFree(L.block);
+		if (L.block) (void)dev_free(L.block);
 	if (ln.levels_pinned) (void)hipHostFree(ln.levels_pinned);
-	if (ln.levels_dev) (void)hipFree(ln.levels_dev);
+	if (ln.levels_dev) (void)dev_free(ln.levels_dev);
 	if (ln.counts_host) (void)hipHostFree(ln.counts_host);
 	for (auto& ev : ln.level_events)
 		for (hipEvent_t e : ev) (void)hipEventDestroy(e);
@@ -929,14 +976,14 @@ struct Render {
 	// now on the device (copy_rows, on the stream the chunk runs on)
 	int prepare_rows(Lane& ln, const std::vector<Segment>& segs, int64_t n_rows, bool* copy) {
 		if (ln.rows_cap < n_rows) {
-			if (ln.rows_dev) HIP_TRY(hipFree(ln.rows_dev));
+			if (ln.rows_dev) HIP_TRY(dev_free(ln.rows_dev));
 			if (ln.rows_pin) HIP_TRY(hipHostFree(ln.rows_pin));
 			ln.rows_dev = nullptr;
 			ln.rows_pin = nullptr;
 			ln.rows_cap = 0;
 			ln.rows_uploaded = -1;
 			const int64_t cap = std::max<int64_t>(n_rows, 1024);
-			HIP_TRY(hipMalloc(reinterpret_cast<void**>(&ln.rows_dev), cap * sizeof(rtamd::ChunkRow)));
+			HIP_TRY(dev_alloc((&ln.rows_dev), cap * sizeof(rtamd::ChunkRow)));
 			HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.rows_pin), cap * sizeof(rtamd::ChunkRow),
 			                      kPinned));
 			ln.rows_cap = cap;
@@ -991,10 +1038,10 @@ struct Render {
 				                       [](const Lane::RowTable& a, const Lane::RowTable& b) { return a.used < b.used; });
 			}
 			if (t->cap < n_rows) {
-				if (t->dev) HIP_TRY(hipFree(t->dev));
+				if (t->dev) HIP_TRY(dev_free(t->dev));
 				t->dev = nullptr;
 				t->cap = 0;
-				HIP_TRY(hipMalloc(reinterpret_cast<void**>(&t->dev), std::max<int64_t>(n_rows, 64) * sizeof(rtamd::ChunkRow)));
+				HIP_TRY(dev_alloc((&t->dev), std::max<int64_t>(n_rows, 64) * sizeof(rtamd::ChunkRow)));
 				t->cap = std::max<int64_t>(n_rows, 64);
 			}
 			// valid only once its upload is queued (start_chunk commits it)
@@ -1492,20 +1539,20 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	s->ds.n_lights = static_cast<int32_t>(fs.lights.size());
 	s->ds.n_nonambient = static_cast<int32_t>(shadow_light.size());
 	void* c = nullptr;
-	HIP_TRY(hipMalloc(&c, sizeof(rtamd::DeviceCounters)));
+	HIP_TRY(dev_alloc(&c, sizeof(rtamd::DeviceCounters)));
 	s->allocs.push_back(c);
 	s->ctr = static_cast<rtamd::DeviceCounters*>(c);
 	void* st = nullptr;
-	HIP_TRY(hipMalloc(&st, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
+	HIP_TRY(dev_alloc(&st, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride));
 	s->allocs.push_back(st);
 	s->stats = static_cast<unsigned long long*>(st);
 	void* fd = nullptr;
-	HIP_TRY(hipMalloc(&fd, kFinDoneBytes));
+	HIP_TRY(dev_alloc(&fd, kFinDoneBytes));
 	s->allocs.push_back(fd);
 	s->fin_done = static_cast<uint32_t*>(fd);
 	HIP_TRY(clear_device(s->fin_done, kFinDoneBytes));
 	void* sm = nullptr;
-	HIP_TRY(hipMalloc(&sm, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1)));
+	HIP_TRY(dev_alloc(&sm, sizeof(unsigned long long) * (rtamd::ST_COUNT + 1)));
 	s->allocs.push_back(sm);
 	s->summary = static_cast<unsigned long long*>(sm);
 	// written by the kernels, read by the host
@@ -1538,9 +1585,9 @@ void rt_scene_destroy(rt_scene* s) {
 	(void)hipSetDevice(s->device);
 	(void)hipDeviceSynchronize();
 	for (auto& ln : s->lanes) lane_destroy(*ln);
-	for (void* p : s->allocs) (void)hipFree(p);
-	if (s->out_dev) (void)hipFree(s->out_dev);
-	if (s->out8_dev) (void)hipFree(s->out8_dev);
+	for (void* p : s->allocs) (void)dev_free(p);
+	if (s->out_dev) (void)dev_free(s->out_dev);
+	if (s->out8_dev) (void)dev_free(s->out8_dev);
 	if (s->mapped_stage) (void)hipHostFree(s->mapped_stage);
 	if (s->summary_host) (void)hipHostFree(s->summary_host);
 	if (s->fork_event) (void)hipEventDestroy(s->fork_event);
@@ -2022,17 +2069,17 @@ void add_counters(rt_counters& a, const rt_counters& b) {
 // whose caller wants RGB8 only: the f64 image is needed for the global maximum)
 int ensure_staging(rt_scene* s, int64_t n_pixels, bool f64, bool u8) {
 	if (f64 && s->out_capacity < n_pixels) {
-		if (s->out_dev) HIP_TRY(hipFree(s->out_dev));
+		if (s->out_dev) HIP_TRY(dev_free(s->out_dev));
 		s->out_dev = nullptr;
 		s->out_capacity = 0;
-		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->out_dev), std::max<int64_t>(n_pixels, 1) * 3 * sizeof(double)));
+		HIP_TRY(dev_alloc((&s->out_dev), std::max<int64_t>(n_pixels, 1) * 3 * sizeof(double)));
 		s->out_capacity = n_pixels;
 	}
 	if (u8 && s->out8_capacity < n_pixels) {
-		if (s->out8_dev) HIP_TRY(hipFree(s->out8_dev));
+		if (s->out8_dev) HIP_TRY(dev_free(s->out8_dev));
 		s->out8_dev = nullptr;
 		s->out8_capacity = 0;
-		HIP_TRY(hipMalloc(reinterpret_cast<void**>(&s->out8_dev), std::max<int64_t>(n_pixels, 1) * 3));
+		HIP_TRY(dev_alloc((&s->out8_dev), std::max<int64_t>(n_pixels, 1) * 3));
 		s->out8_capacity = n_pixels;
 	}
 	return RT_OK;
@@ -2318,6 +2365,36 @@ int rt_debug_rows_verify(rt_scene* s) {
 	return bad;
 }
 
+// Diagnostic (RT_GUARD_BYTES builds): the guard regions a kernel has written into; each
+// corrupted one is described on stderr.  0 without guards.  Not in rtamd.h.
+int rt_debug_guards_check() {
+	std::vector<GuardRegion> v;
+	{
+		std::lock_guard<std::mutex> lk(g_guard_mu);
+		v = guard_regions();
+	}
+	HIP_TRY(hipDeviceSynchronize());
+	int bad = 0;
+	std::vector<unsigned char> back;
+	for (const GuardRegion& g : v) {
+		back.resize(g.bytes);
+		HIP_TRY(hipMemcpy(back.data(), g.at, g.bytes, hipMemcpyDeviceToHost));
+		size_t first = g.bytes, n = 0;
+		for (size_t k = 0; k < g.bytes; k++)
+			if (back[k] != kGuardByte) {
+				if (first == g.bytes) first = k;
+				n++;
+			}
+		if (n) {
+			if (bad < 8)
+				std::fprintf(stderr, "rtamd guard: allocation %p, guard at offset %zu: %zu bytes written, first at +%zu\n",
+				             g.base, g.offset, n, first);
+			bad++;
+		}
+	}
+	return bad;
+}
+
 // Diagnostic: every lane's device level records and row table against their pinned
 // sources; the number of differing records/rows.  Not in rtamd.h.
 int rt_debug_levels_verify(rt_scene* s) {
@@ -2361,10 +2438,10 @@ int rt_selftest_math(int device, int op, const double* x, const double* y, doubl
 		double* p[3] = {nullptr, nullptr, nullptr};
 		~DeviceBuffers() {
 			for (double* q : p)
-				if (q) (void)hipFree(q);
+				if (q) (void)dev_free(q);
 		}
 	} buf;
-	for (double*& q : buf.p) HIP_TRY(hipMalloc(reinterpret_cast<void**>(&q), n * sizeof(double)));
+	for (double*& q : buf.p) HIP_TRY(dev_alloc((&q), n * sizeof(double)));
 	double *dx = buf.p[0], *dy = buf.p[1], *dout = buf.p[2];
 	HIP_TRY(hipMemcpy(dx, x, n * sizeof(double), hipMemcpyHostToDevice));
 	HIP_TRY(hipMemcpy(dy, y ? y : x, n * sizeof(double), hipMemcpyHostToDevice));
@@ -2412,12 +2489,12 @@ int rt_debug_fetch_calibration(int device, int64_t bytes) {
 		void* p[3] = {nullptr, nullptr, nullptr};
 		~Buffers() {
 			for (void* q : p)
-				if (q) (void)hipFree(q);
+				if (q) (void)dev_free(q);
 		}
 	} b;
-	HIP_TRY(hipMalloc(&b.p[0], bytes));
-	HIP_TRY(hipMalloc(&b.p[1], bytes));
-	HIP_TRY(hipMalloc(&b.p[2], 64));
+	HIP_TRY(dev_alloc(&b.p[0], bytes));
+	HIP_TRY(dev_alloc(&b.p[1], bytes));
+	HIP_TRY(dev_alloc(&b.p[2], 64));
 	HIP_TRY(hipMemset(b.p[0], 0, bytes));
 	HIP_TRY(hipMemset(b.p[1], 0, bytes));
 	HIP_TRY(hipDeviceSynchronize());
@@ -2442,10 +2519,10 @@ int rt_debug_valu_calibration(int device, int iters) {
 	struct Sink {
 		void* p = nullptr;
 		~Sink() {
-			if (p) (void)hipFree(p);
+			if (p) (void)dev_free(p);
 		}
 	} sink;
-	HIP_TRY(hipMalloc(&sink.p, 64));
+	HIP_TRY(dev_alloc(&sink.p, 64));
 	for (int kind = 0; kind < 3; kind++)
 		for (int w = 1; w <= 8; w *= 2) {
 			const int it = std::max(1, iters * 8 / w);
@@ -2466,12 +2543,12 @@ int rt_debug_valu_rate(int device, int kind, int waves, int iters, double* ms) {
 		void* p = nullptr;
 		hipEvent_t e0 = nullptr, e1 = nullptr;
 		~Res() {
-			if (p) (void)hipFree(p);
+			if (p) (void)dev_free(p);
 			if (e0) (void)hipEventDestroy(e0);
 			if (e1) (void)hipEventDestroy(e1);
 		}
 	} r;
-	HIP_TRY(hipMalloc(&r.p, 64));
+	HIP_TRY(dev_alloc(&r.p, 64));
 	HIP_TRY(hipEventCreate(&r.e0));
 	HIP_TRY(hipEventCreate(&r.e1));
 	HIP_TRY(rtamd::launch_valu_peak(std::max(1, iters / 4), kind, waves, r.p, nullptr));  // warm-up (clocks)

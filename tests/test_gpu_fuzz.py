@@ -143,6 +143,8 @@ def test_random_scene_matches_oracle(gpu, oracle, tmp_path, seed, monkeypatch):
     if diff:
         raise AssertionError(_diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st))
     _close(s)
+    if os.environ.get("RTAMD_FUZZ_GUARDS") == "1":  # a guard build (RT_GUARD_BYTES): no out-of-bounds write so far
+        assert gpu.lib().rt_debug_guards_check() == 0, f"seed {seed}: a guard region was written"
     assert (st.trace_rays, st.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
 
 
@@ -198,6 +200,7 @@ def _diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st):
     reread = (where, _ndiff(buf, want))
     bad_words, bad_rows = L.rt_debug_scene_verify(s.handle), L.rt_debug_rows_verify(s.handle)
     bad_levels = L.rt_debug_levels_verify(s.handle)
+    guards = L.rt_debug_guards_check() if hasattr(L, "rt_debug_guards_check") else None
     L.rt_debug_invalidate_caches(0)
     after_inv = _ndiff(s.renderScene(options=opts), want)
     st_inv = s.last_stats
@@ -218,7 +221,7 @@ def _diagnose_mismatch(gpu, oracle, s, path, opts, seed, got, want, cnt, st):
             f"oracle on 1 thread vs the first oracle: {_ndiff(want1, want)}; fresh scene vs oracle: "
             f"{_ndiff(fresh, want)}, vs the first render: {_ndiff(fresh, got)}; after a cache invalidation vs "
             f"oracle: {after_inv}; scene block words differing from the upload: {bad_words}; row-table entries "
-            f"differing: {bad_rows}; level records differing (+1000 per chunk row): {bad_levels}; last image read again (where, differing pixels): {reread}; rays "
+            f"differing: {bad_rows}; level records differing (+1000 per chunk row): {bad_levels}; guards written: {guards}; last image read again (where, differing pixels): {reread}; rays "
             f"(trace, shadow, reflect, refract): oracle "
             f"{[cnt[k] for k in ('trace_rays', 'shadow_rays', 'reflect_rays', 'refract_rays')]}, first {_rays(st)}, "
             f"after invalidation {_rays(st_inv)}, fresh {_rays(st_fresh)}")
