@@ -329,6 +329,11 @@ namespace {
 #define RT_PINNED_COHERENT 1
 #endif
 constexpr unsigned kPinned = RT_PINNED_COHERENT ? hipHostMallocCoherent : hipHostMallocDefault;
+// RT_NO_MAPPED=1 (a diagnostic build): no kernel reads or writes host memory: the scene is
+// uploaded by a copy, the summary copied back, and images staged in device memory
+#ifndef RT_NO_MAPPED
+#define RT_NO_MAPPED 0
+#endif
 constexpr unsigned kPinnedMapped = hipHostMallocMapped | (RT_PINNED_COHERENT ? hipHostMallocCoherent : 0u);
 
 // Device allocations.  RT_GUARD_BYTES > 0 (a diagnostic build, tools/build_variant.sh)
@@ -408,7 +413,9 @@ struct UploadBatch {
 		hipError_t e = hipHostGetDevicePointer(&stage_dev, stage, 0);
 		std::memset(stage, 0, total);  // the padding between arrays too (rt_debug_scene_verify)
 		for (const Item& it : items) std::memcpy(static_cast<char*>(stage) + it.offset, it.host, it.bytes);
-		if (e == hipSuccess) e = rtamd::launch_copy16(block, stage_dev, static_cast<int64_t>(total / 16), s->stream);
+		if (e == hipSuccess)
+			e = RT_NO_MAPPED ? hipMemcpyAsync(block, stage, total, hipMemcpyHostToDevice, s->stream)
+			                 : rtamd::launch_copy16(block, stage_dev, static_cast<int64_t>(total / 16), s->stream);
 		if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
 		(void)hipHostFree(stage);
 		if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("scene upload: ") + hipGetErrorString(e));
@@ -1560,7 +1567,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	                      kPinned));
 	{
 		void* mapped = nullptr;
-		if (hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
+		if (!RT_NO_MAPPED && hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
 			s->summary_mapped = static_cast<unsigned long long*>(mapped);
 		(void)hipGetLastError();
 	}
@@ -2097,7 +2104,7 @@ hipError_t copy_to_host(void* dst, const void* src, size_t bytes) {
 // at most kMappedStageMax bytes (f64 + RGB8: a 2560x1600 frame; a 4096^2 f64 image, 400 MB,
 // is copied instead of pinning that much host memory for the scene's lifetime)
 #ifndef RT_MAPPED_STAGE_MAX
-#define RT_MAPPED_STAGE_MAX (size_t(128) << 20)
+#define RT_MAPPED_STAGE_MAX (RT_NO_MAPPED ? size_t(0) : size_t(128) << 20)
 #endif
 constexpr size_t kMappedStageMax = RT_MAPPED_STAGE_MAX;
 int ensure_mapped_stage(rt_scene* s, size_t bytes) {
