@@ -49,6 +49,8 @@ const char* device_error_text(int code) {  // MathException what() (rtbase.h:14-
 		case rtamd::DERR_STACK: return "internal: BVH traversal stack overflow";
 		case rtamd::DERR_ORIGIN_DIRECTION: return "ray origin is a direction vector";
 		case rtamd::DERR_PLAN: return "internal: a replayed launch plan did not fit the render";
+		case rtamd::DERR_ROWS: return "internal: a chunk row descriptor names no selected row of the frame";
+		case rtamd::DERR_RECORD: return "internal: a device level record is not the one uploaded";
 		default: return "unknown device error";
 	}
 }
@@ -60,325 +62,25 @@ namespace rtamd {
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace rtamd
 
-struct rt_builder {
-	rtamd::Scene scene;
-	// rt_builder_get_desc views (rebuilt on every call)
-	std::vector<rt_geometry_desc> desc_geoms;
-	std::vector<rt_light_desc> desc_lights;
-};
+#include "render_state.h"
 
-static_assert(sizeof(rt_face_desc) == sizeof(rtamd::Face) && sizeof(rt_face_desc) == 192,
-              "rt_face_desc is Mesh::Face (geometry.h:32) and the host Face");
-
-// One image (or row selection) of a render call: its parameters and outputs.
-struct Job {
-	const rt_render_params* p;
-	double* out_rgb_dev;
-	uint8_t* out_rgb8_dev;
-	int depth, io;
-	int64_t W, n_rows;
-};
-
-// Rows [r0, r0 + rows) of a job's selected rows (ordinals), part of one chunk
-struct Segment {
-	const Job* job;
-	int64_t r0, rows;
-};
-
-// Progress of a render call (scene.cpp:41-44: the calling thread reports completed pixels
-// about every 100 ms): pixels of the chunks whose output kernel has finished, as seen by
-// the host's event polling.
-struct Progress {
-	rt_progress_fn fn = nullptr;
-	void* user = nullptr;
-	int total = 0;
-	int64_t done = 0;
-	double last = -1.0;
-};
-
-struct LevelBuffers {
-	rtamd::RayLevel lv{};
-	void* block = nullptr;
-	int64_t bytes = 0;
-};
-
-// A chunk shape traced once host-driven becomes a plan: the same launch sequence with every
-// level size read on the device (k_closest's n from the previous level's child counter,
-// the shading batches and reductions from the hit and child counters), issued at once for
-// every later chunk of that shape, with no host round trip between levels.
-// (Capturing that sequence into a hipGraph measured slower on this ROCm: graph replay
-// serialised the branches and the lanes; round 2.)  Levels and
-// capacities come from the traced chunk; a replay that would need more (a deeper level, a
-// larger level) is caught on the device (DERR_PLAN, nothing written past a buffer) and the
-// render is redone host-driven.
-struct PlanKey {
-	int32_t width, height, depth, io;
-	int32_t direct_levels;  // the schedule's split of direct and batched shading (a graph bakes it in)
-	int32_t deep_split;     // levels shaded alone after the chain (per call: single frame or batch)
-	int32_t work_stats;     // the traversal kernels' counting instantiation (a graph bakes it in)
-	int64_t light_major_below;  // shading launches' item layout (per call; a graph bakes it in)
-	int64_t n0;
-	uint64_t rows_hash;  // the chunk's image rows (they decide the level counts)
-	bool operator==(const PlanKey& o) const {
-		return width == o.width && height == o.height && depth == o.depth && io == o.io &&
-		       direct_levels == o.direct_levels && deep_split == o.deep_split && work_stats == o.work_stats &&
-		       light_major_below == o.light_major_below && n0 == o.n0 &&
-		       rows_hash == o.rows_hash;
-	}
-};
-
-// plans kept per lane and shared per scene (oldest dropped first): a batch of one shape has
-// at most 2 x lanes chunk shapes
-constexpr size_t kMaxPlans = 64;
-struct Plan {
-	PlanKey key{};
-	int n_levels = 0;
-	// rays and hits of every level in the traced chunk: they size the grids only (the kernels
-	// read the actual counts and stride over them, so a difference costs time, not results)
-	std::vector<int64_t> level_n, hits;
-	// the level buffer capacities a replay needs (plan sharing, right-sizing): the traced
-	// chunk's ray counts, which a replay of the same key reproduces exactly (same rows, same
-	// scene), not the host-driven trace's one-level-lookahead bounds
-	std::vector<int64_t> capacity;
-	int launches[3] = {0, 0, 0};
-};
-
-// One render pipeline: its own level buffers, streams and events, tracing one chunk of
-// rows (<= 4 M pixels) at a time as a host-polled state machine (Render below).  Several
-// lanes can trace chunks of a frame concurrently (RTAMD_LANES); on C3 one lane is
-// fastest, because every chunk pays the level chain's latency.
-struct Lane {
-	hipStream_t stream = nullptr;        // k_closest chain, reduce, output (high priority)
-	hipStream_t readback = nullptr;      // level counts -> host, off the chain's stream
-	// k_shadow + k_shade of level L < direct_levels on shade[L % 3]; the small deep levels
-	// are shaded in batches on shade[3] once the chain has finished
-	hipStream_t shade[4] = {nullptr, nullptr, nullptr, nullptr};
-	int prio_low = 0;
-	// a scene's first call borrows the scene's stream for everything (chain, read-back,
-	// shading: no stream of its own, each costs 8-15 ms to make); the next call gives the
-	// lane its own (upgrade_lane)
-	bool minimal = false;
-	std::vector<LevelBuffers> levels;
-	// the largest ray count of each level traced host-driven during the current call, and
-	// whether a level buffer grew in it (right_size_levels)
-	std::vector<int64_t> call_need;
-	bool grew = false;
-	// RayLevel records of all levels, read by the kernels through the constant address space
-	// (pinned host copy + device copy, updated in stream order when a level is reallocated)
-	rtamd::RayLevel* levels_pinned = nullptr;
-	rtamd::RayLevel* levels_dev = nullptr;
-	size_t levels_cap = 0;
-	// per level: [0] before k_closest, [1] after it (the shading streams wait on it),
-	// [5] the level's counts copied to counts_host; per shading launch, in the events of
-	// its first level: [2] before k_shadow, [3] after it, [4] after k_shade (the reduce
-	// waits on it)
-	std::vector<std::array<hipEvent_t, 6>> level_events;
-	hipEvent_t chunk_done = nullptr;     // output of the chunk written
-	int32_t* counts_host = nullptr;      // pinned, per level: hits, children (levels_cap x 2)
-	// chunk state
-	enum Phase { IDLE, TRACING, FINISHING } phase = IDLE;
-	std::vector<Segment> segs;            // the chunk's rows: pieces of one or several jobs
-	int depth = 0, io = 0;                // shared by the chunk's jobs
-	uint64_t rows_hash = 0;               // the image rows of the chunk (plan key)
-	rtamd::FrameGeometry fg{};
-	int64_t n0 = 0;                       // pixels of the chunk (its rows x width)
-	rtamd::ChunkRow* rows_dev = nullptr;  // the chunk's row table (device; FrameGeometry::rows)
-	rtamd::ChunkRow* rows_pin = nullptr;  // its pinned staging (one chunk in flight per lane)
-	int64_t rows_cap = 0;
-	int64_t rows_uploaded = -1;           // rows of the table now on the device (-1: none), = rows_pin[0, n)
-	// row tables already on the device, by content (launch plans issued directly, RTAMD_GRAPH 2):
-	// a chunk whose table is among them needs no upload (an H2D copy from pinned memory is a blit
-	// kernel of 30-50 us on the chain's critical path); the lanes of a multi-chunk frame or of a
-	// batch alternate between a few tables
-	struct RowTable {
-		std::vector<rtamd::ChunkRow> host;  // the content (exact comparison)
-		uint64_t hash = 0;
-		rtamd::ChunkRow* dev = nullptr;
-		int64_t cap = 0;
-		uint64_t used = 0;
-	};
-	std::vector<RowTable> tables;
-	uint64_t table_clock = 0;
-	RowTable* table_pending = nullptr;    // the table the current chunk's rows are being copied into
-	uint64_t table_pending_hash = 0;
-	int level = 0;                        // the level whose counts are awaited
-	std::vector<int64_t> level_n;         // ray counts of the levels known so far
-	std::vector<int> shaded;                        // first level of each shading launch
-	std::vector<std::pair<int, int64_t>> deferred;  // (level, hits) shaded after the chain
-	// launch plans of the chunk shapes this lane has traced (plain data: the level buffers are
-	// read from the lane when a plan is issued)
-	std::vector<Plan> plans;
-	const Plan* planned = nullptr;        // the plan replaying the current chunk, if any
-	bool forked = false;                  // this call's caller stream joined into the lane's streams
-	bool direct = false;                  // the current chunk runs on the caller's stream (Render::start_chunk)
-};
-
-void clear_plans(Lane& ln) {
-	ln.plans.clear();
-	ln.planned = nullptr;
-}
-
-struct rt_scene {
-	int device = 0;
-	hipStream_t stream = nullptr;                // default caller stream (rt_render, normalize)
-	rtamd::DeviceScene ds{};
-	std::vector<void*> allocs;
-	// the scene's uploaded block and the bytes staged for it (rt_debug_scene_verify)
-	const void* upload_block = nullptr;
-	std::vector<unsigned char> upload_host;
-	rt_scene_info info{};
-	std::vector<std::unique_ptr<Lane>> lanes;
-	rtamd::DeviceCounters* ctr = nullptr;        // device
-	unsigned long long* stats = nullptr;         // device, kStatShards x kStatStride
-	unsigned long long* summary = nullptr;       // device, ST_COUNT + 1 (k_stats_finish)
-	unsigned long long* summary_host = nullptr;  // pinned mirror
-	// the pinned mirror's device address: k_stats_finish writes the summary straight into host
-	// memory (no copy launch behind it on the call's critical path); null: copy from `summary`
-	unsigned long long* summary_mapped = nullptr;
-	double* out_dev = nullptr;                   // staging for rt_render (f64)
-	int64_t out_capacity = 0;
-	uint8_t* out8_dev = nullptr;                 // staging for rt_render_rgb8
-	void* mapped_stage = nullptr;                // mapped pinned host image (render_to_host)
-	void* mapped_stage_dev = nullptr;
-	size_t mapped_stage_bytes = 0;
-	int64_t out8_capacity = 0;
-	int fail_after = -1;                         // fault injection (rt_debug_fail_after): launches left
-	hipEvent_t fork_event = nullptr;             // caller's stream -> lane streams
-	// RTAMD_DIRECT_LEVELS: levels shaded beside the closest-hit chain; the rest are shaded in
-	// batches after it.  Measured best on C3: 3 for one frame per call
-	// (latency: level 1's shading overlaps levels 2+), 1 for batches (throughput: fewer,
-	// larger shading launches while other frames fill the GPU).  The variable sets both.
-	int direct_levels_single = 3;
-	int direct_levels_batch = 1;
-	int single_lanes = 0;                        // lanes one frame is split over (RTAMD_LANES); 0 = auto
-	// chunk pipelines of a batch in flight (RTAMD_BATCH_LANES).  4 lanes gave the C3 bench
-	// +0.2-1.2%, but single frames rendered after such a batch took 1.31-1.34 instead of
-	// 1.16-1.18 ms (its 24 streams share the process's hardware queues differently); 8 lanes and
-	// smaller chunks lose (profiles/round4/ab/batch_*)
-	int batch_lanes = 3;
-	int prio_low = 0, prio_high = 0;
-	int chunks_per_lane = 2;
-	int serial = 0;                              // RTAMD_SERIAL: shading on the chain's stream (solo kernel times)
-	// launch plans of traced chunk shapes (false while a call whose plan missed is redone
-	// host-driven, render_jobs_once)
-	bool plans = true;
-	int64_t batch_chunk_pixels = (int64_t)1 << 22;  // RTAMD_BATCH_CHUNK: most pixels of a chunk packed from several jobs
-	// plans are plain data: a lane adopts a plan another lane built (growing its level buffers
-	// to the plan's capacities) instead of tracing the chunk shape host-driven itself (+0.7%
-	// whole frames, +1.3% on the 4-way share, round 2)
-	std::vector<Plan> shared_plans;
-	bool force_work_stats = false;               // RTAMD_WORK_STATS: every call counts (rt_render_params::work_stats)
-	int plan_truncate = 0;                       // RTAMD_PLAN_TRUNCATE (tests): plans one level short, replays miss
-	int shadow_all_lights = 3;                   // RTAMD_SHADOW_ALL_LIGHTS: bit 0 level 0, bit 1 deeper (ShadeBatch)
-	// RTAMD_LIGHT_MAJOR_BELOW: a shading launch with fewer hits than this traces light-major
-	// (one lane per (hit, light)) even where the all-lights layout is selected: a few waves per
-	// SIMD each tracing every light in turn leave the GPU latency-bound (one GPU's row share
-	// of a single frame); light-major gives n_lights times the waves, each a shorter chain
-	// Per call like direct_levels: a single frame (or one device's row share of it) of a scene
-	// with meshes traces light-major below 1 M hits (C4 0.401 -> 0.354 ms, C2b 0.349 -> 0.326,
-	// C3 1.284 -> 1.259),
-	// a batch below 128 K (its level-1 launch of 2-frame chunks, ~840 K hits, measured -7% as
-	// light-major, and an 8-way row share -3 to -6%: DESIGN.md §4)
-	int64_t light_major_below_single = (int64_t)1 << 20;
-	int64_t light_major_below_batch = (int64_t)1 << 17;
-	// RTAMD_ONE_STREAM_PIXELS: a replayed chunk of at most this many pixels is issued on one
-	// stream (Render::issue_plan)
-	// (a plan of one traced level is issued on one stream too: it has no deeper level for its
-	// shading to overlap; C4 0.365 -> 0.351 ms, round 3)
-	int64_t one_stream_pixels = (int64_t)1 << 17;
-	// RTAMD_FUSED: a replayed one-stream chunk traces every level in ONE launch (k_fused: closest
-	// hits + shadow rays + Phong terms, and for a plan of one level the output pixels too)
-	// instead of k_closest + k_shadow (+ k_shade) per level and k_output
-	int fused = 1;
-	// RTAMD_FUSED_MIN_PIXELS: a mesh scene's chunk of fewer pixels keeps the split launches.  Such
-	// a chunk is one round of waves, so its time is its slowest tile's; fused, that tile also
-	// traces every light's shadow rays in turn, split the shadow rays are spread over a second
-	// launch of (hit, light) items: the C4 1/8 row share 0.234 -> 0.208 ms, C1-C4 unchanged
-	// (profiles/round4/ab/latency_quad_fuse_knobs.txt)
-	int64_t fused_min_pixels = 524288;
-	// RTAMD_LEVEL_BUDGET: bytes of level buffers all lanes may hold together (0: no limit).  A
-	// render whose host-driven trace would need more is redone with chunks of half as many
-	// pixels (budget_chunk_pixels, kept for later calls) until it fits (render_jobs)
-	int64_t level_budget = 0;
-	int64_t budget_chunk_pixels = 0;
-	int64_t calls = 0;            // render calls so far
-	uint32_t* fin_done = nullptr;  // device: blocks done of a launch that finishes the statistics (9 x 128 B)
-	int all_lights_for(int first_level, int64_t hits, int64_t light_major_below) const {
-		int al = (shadow_all_lights >> (first_level == 0 ? 0 : 1)) & 1;
-		if (al && ds.n_nonambient > 1 && hits < light_major_below) al = 0;
-		return al;
-	}
-	// RTAMD_DEEP_SPLIT: the first n levels after the direct ones are shaded alone, each in
-	// its own launch after the chain, before one batch of the rest (a batch's first bounce
-	// then traces its shadow rays as packets; per call like direct_levels)
-	int deep_split_single = 0;
-	int deep_split_batch = 1;
-	// measured best on C3: packets for the camera rays and their first bounce, and
-	// for the shadow rays of both (once the zero-term decision thinned the per-lane waves)
-	int packet_mask =
-	    rtamd::kPacketClosest0 | rtamd::kPacketClosest1 | rtamd::kPacketShadow0 | rtamd::kPacketShadow1;
-};
 
 namespace {
 
 // Pinned host memory (staging, records, counts, the summary and the mapped image stage):
-// fine-grained (coherent) by default, so that no GPU cache holds a line of it between a
-// kernel's write and the host's read; RT_PINNED_COHERENT=0 builds round 4's coarse-grained
-// allocations (A/B of the cost on the mapped image writes).
-#ifndef RT_PINNED_COHERENT
-#define RT_PINNED_COHERENT 1
-#endif
-constexpr unsigned kPinned = RT_PINNED_COHERENT ? hipHostMallocCoherent : hipHostMallocDefault;
-// RT_NO_MAPPED=1 (a diagnostic build): no kernel reads or writes host memory: the scene is
-// uploaded by a copy, the summary copied back, and images staged in device memory
-#ifndef RT_NO_MAPPED
-#define RT_NO_MAPPED 0
-#endif
-constexpr unsigned kPinnedMapped = hipHostMallocMapped | (RT_PINNED_COHERENT ? hipHostMallocCoherent : 0u);
+// fine-grained (coherent), so that no GPU cache holds a line of it between a kernel's write
+// and the host's read (round 5: no measurable cost on the mapped image writes)
+constexpr unsigned kPinned = hipHostMallocCoherent;
+constexpr unsigned kPinnedMapped = hipHostMallocMapped | hipHostMallocCoherent;
 
-// Device allocations.  RT_GUARD_BYTES > 0 (a diagnostic build, tools/build_variant.sh)
-// follows every allocation, and every array of a level block, with that many bytes of a
-// known pattern; rt_debug_guards_check counts the guards a kernel has written into (an
-// out-of-bounds write of the library's own).
-#ifndef RT_GUARD_BYTES
-#define RT_GUARD_BYTES 0
-#endif
-constexpr size_t kGuard = RT_GUARD_BYTES;
-constexpr unsigned char kGuardByte = 0xA5;
-struct GuardRegion {
-	const void* base;  // the allocation it belongs to
-	char* at;
-	size_t bytes;
-	size_t offset;     // from base
-};
-std::mutex g_guard_mu;
-std::vector<GuardRegion>& guard_regions() {
-	static auto* v = new std::vector<GuardRegion>();
-	return *v;
-}
-hipError_t guard_add(const void* base, char* at, size_t bytes) {
-	hipError_t e = hipMemset(at, kGuardByte, bytes);
-	if (e == hipSuccess) e = hipDeviceSynchronize();
-	std::lock_guard<std::mutex> lk(g_guard_mu);
-	guard_regions().push_back({base, at, bytes, static_cast<size_t>(at - static_cast<const char*>(base))});
-	return e;
-}
 template <typename T>
 hipError_t dev_alloc(T** p, size_t bytes) {
 	void* q = nullptr;
-	hipError_t e = hipMalloc(&q, bytes + kGuard);
+	const hipError_t e = hipMalloc(&q, bytes);
 	*p = static_cast<T*>(q);
-	if (e == hipSuccess && kGuard) e = guard_add(q, static_cast<char*>(q) + bytes, kGuard);
 	return e;
 }
-hipError_t dev_free(void* p) {
-	if (kGuard && p) {
-		std::lock_guard<std::mutex> lk(g_guard_mu);
-		auto& v = guard_regions();
-		v.erase(std::remove_if(v.begin(), v.end(), [p](const GuardRegion& g) { return g.base == p; }), v.end());
-	}
-	return hipFree(p);
-}
+hipError_t dev_free(void* p) { return hipFree(p); }
 
 // The scene's arrays in one device block, filled in one launch from mapped pinned staging
 // (RTAMD_UPLOAD 1): one allocation, no copy engine (its first use in a process costs ~16 ms
@@ -411,11 +113,9 @@ struct UploadBatch {
 		HIP_TRY(hipHostMalloc(&stage, total, kPinnedMapped));
 		void* stage_dev = nullptr;
 		hipError_t e = hipHostGetDevicePointer(&stage_dev, stage, 0);
-		std::memset(stage, 0, total);  // the padding between arrays too (rt_debug_scene_verify)
+		std::memset(stage, 0, total);  // the padding between arrays too
 		for (const Item& it : items) std::memcpy(static_cast<char*>(stage) + it.offset, it.host, it.bytes);
-		if (e == hipSuccess)
-			e = RT_NO_MAPPED ? hipMemcpyAsync(block, stage, total, hipMemcpyHostToDevice, s->stream)
-			                 : rtamd::launch_copy16(block, stage_dev, static_cast<int64_t>(total / 16), s->stream);
+		if (e == hipSuccess) e = rtamd::launch_copy16(block, stage_dev, static_cast<int64_t>(total / 16), s->stream);
 		if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
 		(void)hipHostFree(stage);
 		if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("scene upload: ") + hipGetErrorString(e));
@@ -423,9 +123,6 @@ struct UploadBatch {
 			it.set(static_cast<const char*>(block) + it.offset);
 			s->info.device_bytes += static_cast<int64_t>(it.bytes);
 		}
-		s->upload_block = block;
-		s->upload_host.assign(total, 0);
-		for (const Item& it : items) std::memcpy(s->upload_host.data() + it.offset, it.host, it.bytes);
 		return RT_OK;
 	}
 };
@@ -448,7 +145,7 @@ hipError_t clear_device(void* p, size_t bytes) {
 int64_t level_block_bytes(const rt_scene* s, int64_t n) {
 	const int64_t nl = std::max(1, s->ds.n_nonambient);
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	return 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256 + 29 * static_cast<int64_t>(kGuard);
+	return 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
 }
 
 constexpr int kBudgetMiss = 2;  // internal return code: RTAMD_LEVEL_BUDGET exceeded (render_jobs)
@@ -475,12 +172,9 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	s->info.level_bytes += bytes;
 	s->info.level_bytes_peak = std::max(s->info.level_bytes_peak, s->info.level_bytes);
 	char* p = static_cast<char*>(L.block);
-	std::vector<char*> gaps;  // RT_GUARD_BYTES: the guard after each array
 	auto take = [&](int64_t b) {
 		char* r = p;
 		p += align(b);
-		if (kGuard) gaps.push_back(p);
-		p += static_cast<int64_t>(kGuard);
 		return r;
 	};
 	double** d[21] = {&L.lv.ox, &L.lv.oy, &L.lv.oz, &L.lv.dx,  &L.lv.dy,  &L.lv.dz,  &L.lv.hpx,
@@ -495,9 +189,9 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	L.lv.hinside = reinterpret_cast<uint8_t*>(take(n));
 	L.lv.occl = reinterpret_cast<uint8_t*>(take(n * nl));
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
-	for (char* g : gaps) HIP_TRY(guard_add(L.block, g, kGuard));
 	HIP_TRY(clear_device(L.lv.counts, 4 * sizeof(int32_t)));
 	L.lv.capacity = capacity;
+	L.lv.tag = rtamd::level_tag(static_cast<int>(level));
 	return RT_OK;
 }
 
@@ -584,10 +278,6 @@ int lane_create(Lane& ln, int prio_low, int prio_high) {
 
 void lane_destroy(Lane& ln) {
 	clear_plans(ln);
-	if (ln.rows_dev) (void)dev_free(ln.rows_dev);
-	if (ln.rows_pin) (void)hipHostFree(ln.rows_pin);
-	for (auto& t : ln.tables)
-		if (t.dev) (void)dev_free(t.dev);
 	for (auto& L : ln.levels)
 		if (L.block) (void)dev_free(L.block);
 	if (ln.levels_pinned) (void)hipHostFree(ln.levels_pinned);
@@ -720,7 +410,7 @@ struct Render {
 		if (nl > 0) cnt.stage_launches[1]++;
 		HIP_TRY(hipEventRecord(ev[3], q));
 		if (!b.fused) {
-			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
+			HIP_TRY(rtamd::launch_shade(s->ds, b, ln.levels_dev, s->ctr, q));
 			cnt.stage_launches[2]++;
 		}
 		HIP_TRY(hipEventRecord(ev[4], q));
@@ -776,7 +466,7 @@ struct Render {
 		HIP_TRY(rtamd::launch_shadow(s->ds, b, ln.levels_dev, s->ctr, s->stats, q, s->packet_mask));
 		if (nl > 0) pl.launches[1]++;
 		if (!b.fused) {
-			HIP_TRY(rtamd::launch_shade(s->ds, ln.fg, b, ln.levels_dev, s->ctr, q));
+			HIP_TRY(rtamd::launch_shade(s->ds, b, ln.levels_dev, s->ctr, q));
 			pl.launches[2]++;
 		}
 		return RT_OK;
@@ -978,88 +668,44 @@ struct Render {
 		return nullptr;
 	}
 
-	// the chunk's row table: image row and output rows of every selected row of its pieces,
-	// staged in pinned memory (and hashed for the plan key); *copy: it differs from the table
-	// now on the device (copy_rows, on the stream the chunk runs on)
-	int prepare_rows(Lane& ln, const std::vector<Segment>& segs, int64_t n_rows, bool* copy) {
-		if (ln.rows_cap < n_rows) {
-			if (ln.rows_dev) HIP_TRY(dev_free(ln.rows_dev));
-			if (ln.rows_pin) HIP_TRY(hipHostFree(ln.rows_pin));
-			ln.rows_dev = nullptr;
-			ln.rows_pin = nullptr;
-			ln.rows_cap = 0;
-			ln.rows_uploaded = -1;
-			const int64_t cap = std::max<int64_t>(n_rows, 1024);
-			HIP_TRY(dev_alloc((&ln.rows_dev), cap * sizeof(rtamd::ChunkRow)));
-			HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ln.rows_pin), cap * sizeof(rtamd::ChunkRow),
-			                      kPinned));
-			ln.rows_cap = cap;
-		}
+	// The chunk's rows as by-value descriptors (FrameGeometry::seg, one per piece: the kernels
+	// compute each row's image row and output address from them, trace.hip chunk_row), and the
+	// hash of its image rows for the plan key.  plan_chunks never packs more than
+	// kMaxRowSegments pieces into a chunk.
+	int describe_rows(Lane& ln, const std::vector<Segment>& segs, int64_t n_rows) {
+		if (segs.empty() || segs.size() > static_cast<size_t>(rtamd::kMaxRowSegments))
+			return fail(RT_ERR_DEVICE, "internal: a chunk of " + std::to_string(segs.size()) + " row segments");
+		rtamd::FrameGeometry& fg = ln.fg;
+		const Job& first = *segs.front().job;
+		fg = rtamd::FrameGeometry{};
+		fg.width = first.p->width;
+		fg.height = first.p->height;
+		fg.intersection_only = first.io;
+		fg.n_rows = static_cast<int32_t>(n_rows);
+		fg.n_segs = static_cast<int32_t>(segs.size());
 		uint64_t h = 1469598103934665603ull;
 		int64_t q = 0;
-		// the table is rewritten in place; a render call repeating the lane's previous chunk (the
-		// same rows into the same buffers: a frame rendered again) finds it already on the device
-		// and skips the copy (a blit launch on the chain's critical path)
-		bool same = ln.rows_uploaded == n_rows;
-		for (const Segment& sg : segs) {
+		for (size_t k = 0; k < segs.size(); k++) {
+			const Segment& sg = segs[k];
 			const Job& job = *sg.job;
 			const rt_render_params* p = job.p;
-			for (int64_t k = 0; k < sg.rows; k++, q++) {
-				const int64_t ord = sg.r0 + k;  // the job's selected-row ordinal: its output row
-				rtamd::ChunkRow r{};
-				r.row = selected_row(p, ord);
-				r.pad = 0;
-				r.out = job.out_rgb_dev ? job.out_rgb_dev + ord * job.W * 3 : nullptr;
-				r.out8 = job.out_rgb8_dev ? job.out_rgb8_dev + ord * job.W * 3 : nullptr;
-				rtamd::ChunkRow& dst = ln.rows_pin[q];
-				same = same && dst.row == r.row && dst.out == r.out && dst.out8 == r.out8;
-				dst = r;
-				h = (h ^ static_cast<uint32_t>(r.row)) * 1099511628211ull;
-			}
+			rtamd::RowSegment& d = fg.seg[k];
+			d.out = job.out_rgb_dev;
+			d.out8 = job.out_rgb8_dev;
+			d.q0 = static_cast<int32_t>(q);
+			d.ord0 = static_cast<int32_t>(sg.r0);
+			d.ord_end = static_cast<int32_t>(job.n_rows);
+			d.row_begin = p->row_begin;
+			d.row_block = std::max(1, p->row_block);
+			d.row_span = p->row_step * d.row_block;
+			for (int64_t r = 0; r < sg.rows; r++) h = (h ^ static_cast<uint32_t>(selected_row(p, sg.r0 + r))) * 1099511628211ull;
+			q += sg.rows;
 		}
 		ln.rows_hash = h;
-		*copy = !same;
-		ln.rows_uploaded = n_rows;
-		ln.fg.rows = ln.rows_dev;
-		// the content's table among the lane's cached ones, else a new (or the least recently
-		// used) one takes it; *copy then says whether that table must be uploaded
-		uint64_t hc = 1469598103934665603ull;
-		const unsigned char* bytes = reinterpret_cast<const unsigned char*>(ln.rows_pin);
-		for (int64_t k = 0; k < n_rows * static_cast<int64_t>(sizeof(rtamd::ChunkRow)); k++)
-			hc = (hc ^ bytes[k]) * 1099511628211ull;
-		constexpr size_t kMaxTables = 64;
-		ln.tables.reserve(kMaxTables);  // table_pending points into it: never reallocated
-		ln.table_pending = nullptr;
-		Lane::RowTable* t = nullptr;
-		for (auto& c : ln.tables)
-			if (c.hash == hc && static_cast<int64_t>(c.host.size()) == n_rows &&
-			    std::memcmp(c.host.data(), ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow)) == 0)
-				t = &c;
-		*copy = t == nullptr;
-		if (!t) {
-			if (ln.tables.size() < kMaxTables) {
-				ln.tables.emplace_back();
-				t = &ln.tables.back();
-			} else {
-				t = &*std::min_element(ln.tables.begin(), ln.tables.end(),
-				                       [](const Lane::RowTable& a, const Lane::RowTable& b) { return a.used < b.used; });
-			}
-			if (t->cap < n_rows) {
-				if (t->dev) HIP_TRY(dev_free(t->dev));
-				t->dev = nullptr;
-				t->cap = 0;
-				HIP_TRY(dev_alloc((&t->dev), std::max<int64_t>(n_rows, 64) * sizeof(rtamd::ChunkRow)));
-				t->cap = std::max<int64_t>(n_rows, 64);
-			}
-			// valid only once its upload is queued (start_chunk commits it)
-			t->host.clear();
-			t->hash = 0;
-			ln.table_pending = t;
-			ln.table_pending_hash = hc;
+		if (s->corrupt_rows) {  // test hook (rt_debug_corrupt_rows): rows no frame has
+			fg.seg[0].row_begin += fg.height;
+			s->corrupt_rows = 0;
 		}
-		t->used = ++ln.table_clock;
-		ln.fg.rows = t->dev;
-		ln.rows_uploaded = -1;  // rows_dev is not the chunk's table
 		return RT_OK;
 	}
 
@@ -1072,15 +718,8 @@ struct Render {
 		ln.depth = first.depth;
 		ln.io = first.io;
 		ln.n0 = n_rows * first.W;
-		bool copy_rows = false;
-		int rc = prepare_rows(ln, segs, n_rows, &copy_rows);
+		int rc = describe_rows(ln, segs, n_rows);
 		if (rc) return rc;
-		const rtamd::ChunkRow* rows = ln.fg.rows;  // prepare_rows: the chunk's row table
-		ln.fg = rtamd::FrameGeometry{};
-		ln.fg.width = first.p->width;
-		ln.fg.height = first.p->height;
-		ln.fg.intersection_only = first.io;
-		ln.fg.rows = rows;
 		ln.level = 0;
 		ln.level_n.assign(1, ln.n0);
 		ln.shaded.clear();
@@ -1093,14 +732,6 @@ struct Render {
 		ln.direct = direct_ok && pl;
 		const hipStream_t st = ln.direct ? caller : ln.stream;
 		if (!ln.direct && (rc = fork(ln))) return rc;
-		if (copy_rows)
-			HIP_TRY(hipMemcpyAsync(const_cast<rtamd::ChunkRow*>(ln.fg.rows), ln.rows_pin, n_rows * sizeof(rtamd::ChunkRow),
-			                       hipMemcpyHostToDevice, st));
-		if (ln.table_pending) {  // its upload is queued ahead of every kernel that reads it
-			ln.table_pending->host.assign(ln.rows_pin, ln.rows_pin + n_rows);
-			ln.table_pending->hash = ln.table_pending_hash;
-			ln.table_pending = nullptr;
-		}
 		if (!pl && (pl = adopt_plan(ln, key_of(ln), rc), rc)) return rc;
 		if (pl) {
 			if (s->fail_after >= 0 && s->fail_after-- == 0) return fail(RT_ERR_DEVICE, "injected failure (rt_debug_fail_after)");
@@ -1567,7 +1198,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	                      kPinned));
 	{
 		void* mapped = nullptr;
-		if (!RT_NO_MAPPED && hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
+		if (hipHostGetDevicePointer(&mapped, s->summary_host, 0) == hipSuccess)
 			s->summary_mapped = static_cast<unsigned long long*>(mapped);
 		(void)hipGetLastError();
 	}
@@ -1607,6 +1238,7 @@ int rt_scene_get_info(const rt_scene* s, rt_scene_info* info) {
 	*info = s->info;
 	return RT_OK;
 }
+
 }  // extern "C"
 
 namespace {
@@ -1625,18 +1257,17 @@ void reset_after_error(rt_scene* s) {
 	for (auto& ln : s->lanes) {
 		ln->phase = Lane::IDLE;
 		ln->segs.clear();
-		ln->rows_uploaded = -1;
-		ln->table_pending = nullptr;
-		for (auto& t : ln->tables) {  // forget the cached contents (an upload may have failed)
-			t.host.clear();
-			t.hash = 0;
-		}
 		ln->level = 0;
 		ln->level_n.clear();
 		ln->shaded.clear();
 		ln->deferred.clear();
 		for (auto& L : ln->levels)
 			if (L.block) (void)hipMemset(L.lv.counts, 0, 2 * sizeof(int32_t));
+		// the device copy of the level records again from the pinned one (a render that found a
+		// record not the one uploaded fails with DERR_RECORD; the next one starts from the source)
+		if (ln->levels_dev && ln->levels_cap)
+			(void)hipMemcpy(ln->levels_dev, ln->levels_pinned, ln->levels_cap * sizeof(rtamd::RayLevel),
+			                hipMemcpyHostToDevice);
 	}
 	(void)hipMemset(s->stats, 0, sizeof(unsigned long long) * rtamd::kStatShards * rtamd::kStatStride);
 	(void)hipMemset(s->ctr, 0, sizeof(rtamd::DeviceCounters));
@@ -1663,6 +1294,7 @@ int right_size_levels(rt_scene* s) {
 		Lane& ln = *lp;
 		if (!ln.grew) continue;
 		ln.grew = false;
+		bool resized = false;
 		std::vector<int64_t> need = ln.call_need;
 		need.resize(ln.levels.size(), 0);
 		for (const Plan& pl : ln.plans)
@@ -1675,15 +1307,20 @@ int right_size_levels(rt_scene* s) {
 			int rc = alloc_level(s, ln, L, target);
 			if (!rc) rc = ensure_level_record(s, ln, L, 0);  // the device copy of its RayLevel record
 			if (rc) return rc;
+			resized = true;
 		}
 		ln.call_need.clear();
+		// the record copies were queued on the lane's stream; the next call's replay may run on the
+		// caller's stream (Render::start_chunk, Lane::direct), which does not wait for it: they
+		// complete here, before this call returns
+		if (resized) HIP_TRY(hipStreamSynchronize(ln.stream));
 	}
 	return RT_OK;
 }
 
 // RTAMD_LEVEL_BUDGET exceeded: the call's work is dropped, every level buffer freed and the
 // chunks halved (kept for later calls); fails when even small chunks do not fit
-int shrink_for_budget(rt_scene* s, int64_t first_chunk_pixels) {
+int shrink_for_budget(rt_scene* s) {
 	reset_after_error(s);
 	for (auto& lp : s->lanes) {
 		Lane& ln = *lp;
@@ -1697,7 +1334,10 @@ int shrink_for_budget(rt_scene* s, int64_t first_chunk_pixels) {
 		ln.grew = false;
 	}
 	s->shared_plans.clear();
-	const int64_t cur = s->budget_chunk_pixels > 0 ? s->budget_chunk_pixels : first_chunk_pixels;
+	// halved from the largest chunk the failed call planned (halving a larger nominal chunk size
+	// might not change its chunks at all: another full render for nothing)
+	const int64_t cur = s->budget_chunk_pixels > 0 ? std::min(s->budget_chunk_pixels, s->last_chunk_pixels)
+	                                               : s->last_chunk_pixels;
 	const int64_t next = cur / 2;
 	if (next < kMinBudgetChunkPixels)
 		return fail(RT_ERR_DEVICE, "the level buffers of a " + std::to_string(cur) +
@@ -1712,10 +1352,7 @@ int render_jobs(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_coun
 	for (;;) {
 		rc = render_jobs_once(s, jobs, caller, counters, progress);
 		if (rc != kBudgetMiss) break;
-		int64_t first = (int64_t)1 << 22;
-		for (const Job& j : jobs)
-			if (j.p->chunk_pixels > 0) first = std::min<int64_t>(first, j.p->chunk_pixels);
-		if ((rc = shrink_for_budget(s, first))) break;
+		if ((rc = shrink_for_budget(s))) break;
 		if (progress) progress->done = 0;
 	}
 	if (rc == RT_OK) rc = right_size_levels(s);
@@ -1748,6 +1385,8 @@ int render_jobs_once(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	return rc;
 }
 
+}  // namespace
+
 // The chunks of a render call: every job's selected rows as segments, packed into chunks
 // (render_jobs_impl; rt_debug_plan_chunks exposes it to the CPU tests).
 // pixels of a job's chunks: its chunk_pixels (0: 4 M), at most max_chunk_pixels (> 0: the
@@ -1759,13 +1398,14 @@ int64_t chunk_limit(const rt_render_params* p, int64_t max_chunk_pixels) {
 
 std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size_t n_lanes, bool batch,
                                               int64_t batch_chunk_pixels, int batch_balance, int chunks_per_lane,
-                                              int64_t max_chunk_pixels = 0) {
+                                              int64_t max_chunk_pixels) {
 	// Pieces: every job's selected rows cut into pieces of at most its chunk size (4 M
 	// pixels by default: it bounds the level buffers); one image over several lanes is cut
 	// so that every lane holds `chunks_per_lane` of its pieces.  Consecutive pieces of
 	// different jobs with equal width, height, depth and io are packed into one chunk, up to
 	// batch_chunk_pixels: rows of several frames traced as one wavefront (a GPU's share of
-	// row-partitioned frames is a few rows of each frame).
+	// row-partitioned frames is a few rows of each frame).  A chunk holds at most
+	// kMaxRowSegments pieces: its rows are described by value in the kernel arguments.
 	std::vector<std::vector<Segment>> chunks;
 	// Balanced batches (RTAMD_BATCH_BALANCE): jobs of one shape that make fewer than two
 	// chunks per lane are cut into equal chunks whose number is a multiple of the lane count,
@@ -1802,7 +1442,7 @@ std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size
 				cur.push_back(Segment{&job, r0, take});
 				r0 += take;
 				cur_rows += take;
-				if (cur_rows == bal_rows) {
+				if (cur_rows == bal_rows || cur.size() == static_cast<size_t>(rtamd::kMaxRowSegments)) {
 					chunks.push_back(cur);
 					cur.clear();
 					cur_rows = 0;
@@ -1825,7 +1465,7 @@ std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size
 				if (!cur.empty()) {
 					const Job& f = *cur.front().job;
 					fits = cur.back().job != &job && f.p->width == p->width && f.p->height == p->height &&
-					       f.depth == job.depth && f.io == job.io &&
+					       f.depth == job.depth && f.io == job.io && cur.size() < static_cast<size_t>(rtamd::kMaxRowSegments) &&
 					       cur_px + px <= std::min({cur_limit, limit_px, batch_chunk_pixels});
 				}
 				if (!fits && !cur.empty()) {
@@ -1842,6 +1482,8 @@ std::vector<std::vector<Segment>> plan_chunks(const std::vector<Job>& jobs, size
 	}
 	return chunks;
 }
+
+namespace {
 
 int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt_counters* counters,
                      Progress* progress) {
@@ -1895,6 +1537,12 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	const std::vector<std::vector<Segment>> chunks =
 	    plan_chunks(jobs, n_lanes, batch, s->batch_chunk_pixels, 1, chunks_per_lane, s->budget_chunk_pixels);
 	R.direct_ok = n_lanes == 1 && chunks.size() == 1;
+	s->last_chunk_pixels = 0;
+	for (const auto& c : chunks) {
+		int64_t px = 0;
+		for (const Segment& sg : c) px += sg.rows * sg.job->W;
+		s->last_chunk_pixels = std::max(s->last_chunk_pixels, px);
+	}
 	size_t next_chunk = 0;
 	std::unique_ptr<rtamd::MarkerRange> trace_range(new rtamd::MarkerRange("rtamd: trace (levels, shading, output)"));
 	// The statistics reduction is queued on the caller's stream, behind every lane's last
@@ -1956,8 +1604,12 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	if (!stats_issued && (rc = issue_stats())) return rc;
 	HIP_TRY(hipStreamSynchronize(caller));
 	const unsigned long long* sum = s->summary_host;
-	if (sum[rtamd::ST_COUNT] == rtamd::DERR_PLAN) return kPlanMiss;
-	if (sum[rtamd::ST_COUNT]) return fail(RT_ERR_MATH, device_error_text(static_cast<int>(sum[rtamd::ST_COUNT])));
+	const int derr = static_cast<int>(sum[rtamd::ST_COUNT]);
+	if (derr == rtamd::DERR_PLAN) return kPlanMiss;
+	// MathException texts (rtbase.h:14-22) are the reference's; the internal checks are device failures
+	if (derr == rtamd::DERR_STACK || derr == rtamd::DERR_ROWS || derr == rtamd::DERR_RECORD)
+		return fail(RT_ERR_DEVICE, device_error_text(derr));
+	if (derr) return fail(RT_ERR_MATH, device_error_text(derr));
 	rt_counters& cnt = R.cnt;
 	cnt.trace_rays = static_cast<int64_t>(sum[rtamd::ST_RAYS]);
 	cnt.shadow_rays = static_cast<int64_t>(sum[rtamd::ST_HITS]) * s->ds.n_nonambient;
@@ -2000,6 +1652,8 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	return RT_OK;
 }
 
+}  // namespace
+
 Job make_job(const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_dev) {
 	Job j{};
 	j.p = p;
@@ -2012,35 +1666,8 @@ Job make_job(const rt_render_params* p, double* out_rgb_dev, uint8_t* out_rgb8_d
 	return j;
 }
 
-// CPU test hook (tests/test_host.py): the chunks a render call cuts `n` jobs into over
-// `n_lanes` lanes (rt_render_batch_device: n_lanes = min(n, batch lanes)).  Segment k of
-// the plan is out[4k..4k+3] = (chunk, job index in params, first row ordinal, rows); returns
-// the number of segments, or -1 when out_cap segments do not suffice.  Needs no device.
-extern "C" int rt_debug_plan_chunks(int n, const rt_render_params* params, int n_lanes, int64_t batch_chunk_pixels,
-                                    int balance, int64_t* out, int out_cap) {
-	std::vector<Job> jobs;
-	std::vector<int> index;
-	for (int k = 0; k < n; k++) {
-		const Job j = make_job(params + k, nullptr, nullptr);
-		if (j.n_rows <= 0) continue;
-		jobs.push_back(j);
-		index.push_back(k);
-	}
-	if (jobs.empty()) return 0;
-	const auto chunks = plan_chunks(jobs, static_cast<size_t>(std::max(1, n_lanes)), jobs.size() > 1,
-	                                batch_chunk_pixels, balance, 2);
-	int q = 0;
-	for (size_t c = 0; c < chunks.size(); c++)
-		for (const Segment& sg : chunks[c]) {
-			if (q >= out_cap) return -1;
-			out[4 * q] = static_cast<int64_t>(c);
-			out[4 * q + 1] = index[sg.job - jobs.data()];
-			out[4 * q + 2] = sg.r0;
-			out[4 * q + 3] = sg.rows;
-			q++;
-		}
-	return q;
-}
+namespace {
+
 
 void add_counters(rt_counters& a, const rt_counters& b) {
 	a.trace_rays += b.trace_rays;
@@ -2104,7 +1731,7 @@ hipError_t copy_to_host(void* dst, const void* src, size_t bytes) {
 // at most kMappedStageMax bytes (f64 + RGB8: a 2560x1600 frame; a 4096^2 f64 image, 400 MB,
 // is copied instead of pinning that much host memory for the scene's lifetime)
 #ifndef RT_MAPPED_STAGE_MAX
-#define RT_MAPPED_STAGE_MAX (RT_NO_MAPPED ? size_t(0) : size_t(128) << 20)
+#define RT_MAPPED_STAGE_MAX (size_t(128) << 20)
 #endif
 constexpr size_t kMappedStageMax = RT_MAPPED_STAGE_MAX;
 int ensure_mapped_stage(rt_scene* s, size_t bytes) {
@@ -2299,144 +1926,6 @@ int rt_write_png(const char* path, const uint8_t* rgb, int width, int height) {
 	return RT_OK;
 }
 
-// Diagnostic: phase profile of the traversal kernels (RT_PHASE_PROF builds; zeros otherwise),
-// 4 x 8 sums of per-lane shader-clock cycles (trace.h), read and cleared.  Not in rtamd.h.
-int rt_debug_phase_profile(int device, unsigned long long* out32) {
-	HIP_TRY(hipSetDevice(device));
-	HIP_TRY(hipDeviceSynchronize());
-	HIP_TRY(rtamd::read_phase_profile(out32));
-	return RT_OK;
-}
-
-// Diagnostic: the per-wave timing records of an RT_DIAG_WAVETIME build (tools/wave_times.py;
-// 32 B each: t0, t1 on the 100 MHz clock, tag, first item, node iterations, face tests), at
-// most max_records, read and cleared; returns the count (0 in other builds).  Not in rtamd.h.
-int rt_debug_wave_times(int device, void* out, int max_records) {
-	HIP_TRY(hipSetDevice(device));
-	HIP_TRY(hipDeviceSynchronize());
-	const int n = rtamd::read_wave_times(out, max_records);
-	if (n < 0) return fail(RT_ERR_DEVICE, "wave time read-back failed");
-	return n;
-}
-
-// Diagnostic: the scene's device block read back and compared with the bytes staged for it:
-// the number of differing 16-B words (0: intact).
-// Not in rtamd.h.
-int rt_debug_scene_verify(rt_scene* s) {
-	if (!s) return fail(RT_ERR_ARG, "null scene");
-	if (!s->upload_block) return 0;
-	HIP_TRY(hipSetDevice(s->device));
-	HIP_TRY(hipDeviceSynchronize());
-	std::vector<unsigned char> back(s->upload_host.size());
-	HIP_TRY(hipMemcpy(back.data(), s->upload_block, back.size(), hipMemcpyDeviceToHost));
-	int bad = 0;
-	for (size_t w = 0; w + 16 <= back.size(); w += 16)
-		bad += std::memcmp(back.data() + w, s->upload_host.data() + w, 16) != 0;
-	return bad;
-}
-
-// Diagnostic: the last host-image render's f64 image read again from where the kernels wrote
-// it (the mapped stage, else the device staging image), after a device synchronisation.
-// Not in rtamd.h.
-int rt_debug_read_stage(rt_scene* s, double* out, int64_t n_values) {
-	if (!s || !out) return fail(RT_ERR_ARG, "null scene or output");
-	HIP_TRY(hipSetDevice(s->device));
-	HIP_TRY(hipDeviceSynchronize());
-	const size_t bytes = static_cast<size_t>(n_values) * sizeof(double);
-	if (s->mapped_stage && s->mapped_stage_bytes >= bytes) {
-		std::memcpy(out, s->mapped_stage, bytes);
-		return 1;
-	}
-	if (s->out_dev) {
-		HIP_TRY(hipMemcpy(out, s->out_dev, bytes, hipMemcpyDeviceToHost));
-		return 2;
-	}
-	return 0;
-}
-
-// Diagnostic: every lane's cached row tables read back and compared with their host copies:
-// the number of rows that differ.  Not in rtamd.h.
-int rt_debug_rows_verify(rt_scene* s) {
-	if (!s) return fail(RT_ERR_ARG, "null scene");
-	HIP_TRY(hipSetDevice(s->device));
-	HIP_TRY(hipDeviceSynchronize());
-	int bad = 0;
-	for (auto& lp : s->lanes)
-		for (const auto& t : lp->tables) {
-			if (!t.dev || t.host.empty()) continue;
-			std::vector<rtamd::ChunkRow> back(t.host.size());
-			HIP_TRY(hipMemcpy(back.data(), t.dev, back.size() * sizeof(rtamd::ChunkRow), hipMemcpyDeviceToHost));
-			for (size_t k = 0; k < back.size(); k++)
-				bad += std::memcmp(&back[k], &t.host[k], sizeof(rtamd::ChunkRow)) != 0;
-		}
-	return bad;
-}
-
-// Diagnostic (RT_GUARD_BYTES builds): the guard regions a kernel has written into; each
-// corrupted one is described on stderr.  0 without guards.  Not in rtamd.h.
-int rt_debug_guards_check() {
-	std::vector<GuardRegion> v;
-	{
-		std::lock_guard<std::mutex> lk(g_guard_mu);
-		v = guard_regions();
-	}
-	HIP_TRY(hipDeviceSynchronize());
-	int bad = 0;
-	std::vector<unsigned char> back;
-	for (const GuardRegion& g : v) {
-		back.resize(g.bytes);
-		HIP_TRY(hipMemcpy(back.data(), g.at, g.bytes, hipMemcpyDeviceToHost));
-		size_t first = g.bytes, n = 0;
-		for (size_t k = 0; k < g.bytes; k++)
-			if (back[k] != kGuardByte) {
-				if (first == g.bytes) first = k;
-				n++;
-			}
-		if (n) {
-			if (bad < 8)
-				std::fprintf(stderr, "rtamd guard: allocation %p, guard at offset %zu: %zu bytes written, first at +%zu\n",
-				             g.base, g.offset, n, first);
-			bad++;
-		}
-	}
-	return bad;
-}
-
-// Diagnostic: every lane's device level records and row table against their pinned
-// sources; the number of differing records/rows.  Not in rtamd.h.
-int rt_debug_levels_verify(rt_scene* s) {
-	if (!s) return fail(RT_ERR_ARG, "null scene");
-	HIP_TRY(hipSetDevice(s->device));
-	HIP_TRY(hipDeviceSynchronize());
-	int bad = 0;
-	for (auto& lp : s->lanes) {
-		const Lane& ln = *lp;
-		if (ln.levels_dev && ln.levels_cap) {
-			std::vector<rtamd::RayLevel> back(ln.levels_cap);
-			HIP_TRY(hipMemcpy(back.data(), ln.levels_dev, back.size() * sizeof(rtamd::RayLevel), hipMemcpyDeviceToHost));
-			for (size_t k = 0; k < back.size(); k++)
-				bad += std::memcmp(&back[k], &ln.levels_pinned[k], sizeof(rtamd::RayLevel)) != 0;
-		}
-		if (ln.rows_dev && ln.rows_pin && ln.rows_uploaded > 0) {
-			std::vector<rtamd::ChunkRow> back(static_cast<size_t>(ln.rows_uploaded));
-			HIP_TRY(hipMemcpy(back.data(), ln.rows_dev, back.size() * sizeof(rtamd::ChunkRow), hipMemcpyDeviceToHost));
-			for (size_t k = 0; k < back.size(); k++)
-				bad += 1000 * (std::memcmp(&back[k], &ln.rows_pin[k], sizeof(rtamd::ChunkRow)) != 0);
-		}
-	}
-	return bad;
-}
-
-// Diagnostic: a system-scope cache invalidation on every XCD (L2 and L1 non-coherent lines
-// dropped), synchronised.  Not in rtamd.h.
-int rt_debug_invalidate_caches(int device) {
-	HIP_TRY(hipSetDevice(device));
-	HIP_TRY(hipDeviceSynchronize());
-	HIP_TRY(rtamd::launch_invalidate_caches(nullptr));
-	HIP_TRY(hipDeviceSynchronize());
-	return RT_OK;
-}
-
 int rt_selftest_math(int device, int op, const double* x, const double* y, double* out, int64_t n) {
 	if (n <= 0) return RT_OK;
 	if (!x || !out) return fail(RT_ERR_ARG, "null input or output");
@@ -2454,127 +1943,6 @@ int rt_selftest_math(int device, int op, const double* x, const double* y, doubl
 	HIP_TRY(hipMemcpy(dy, y ? y : x, n * sizeof(double), hipMemcpyHostToDevice));
 	HIP_TRY(rtamd::launch_selftest_math(op, dx, dy, dout, n, nullptr));
 	HIP_TRY(hipMemcpy(out, dout, n * sizeof(double), hipMemcpyDeviceToHost));
-	return RT_OK;
-}
-
-// Diagnostic (not in rtamd.h): FNV-1a digest of everything rt_scene_create would upload
-// for the builder's scene (flattened geometry, LBVHs, materials, lights, camera), computed
-// on the host only: equal digests = identical device scenes (tests of rt_builder_set_desc).
-int rt_debug_builder_digest(const rt_builder* b, uint64_t* out) {
-	if (!b || !out) return fail(RT_ERR_ARG, "null builder or output");
-	const rtamd::FlatScene fs = rtamd::flatten_scene(b->scene);
-	uint64_t h = 1469598103934665603ull;
-	auto mix = [&](const void* p, size_t n) {
-		const unsigned char* c = static_cast<const unsigned char*>(p);
-		for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
-	};
-	auto vec = [&](const auto& v) {
-		const uint64_t n = v.size();
-		mix(&n, sizeof(n));
-		if (n) mix(v.data(), n * sizeof(v[0]));
-	};
-	vec(fs.geoms);
-	vec(fs.materials);
-	vec(fs.lights);
-	vec(fs.face_geo);
-	vec(fs.face_nrm);
-	vec(fs.nodes);
-	vec(fs.shadow_order);
-	mix(&fs.camera, sizeof(fs.camera));
-	*out = h;
-	return RT_OK;
-}
-
-// Diagnostic (not in rtamd.h): FETCH_SIZE calibration.  Reads a fresh `bytes` buffer once per
-// width in {1, 4, 8, 16} bytes per lane (one k_stream_read dispatch each, after a dispatch
-// that streams another buffer of the same size through the caches); profiled with
-// rocprofv3 --pmc FETCH_SIZE, the ratio of the counter to `bytes` per width corrects the
-// path's own loads (tools/make_traffic.py).
-int rt_debug_fetch_calibration(int device, int64_t bytes) {
-	HIP_TRY(hipSetDevice(device));
-	struct Buffers {
-		void* p[3] = {nullptr, nullptr, nullptr};
-		~Buffers() {
-			for (void* q : p)
-				if (q) (void)dev_free(q);
-		}
-	} b;
-	HIP_TRY(dev_alloc(&b.p[0], bytes));
-	HIP_TRY(dev_alloc(&b.p[1], bytes));
-	HIP_TRY(dev_alloc(&b.p[2], 64));
-	HIP_TRY(hipMemset(b.p[0], 0, bytes));
-	HIP_TRY(hipMemset(b.p[1], 0, bytes));
-	HIP_TRY(hipDeviceSynchronize());
-	const int widths[4] = {1, 4, 8, 16};
-	for (int w : widths) {
-		// evict: stream the other buffer first (larger than the 256 MiB Infinity Cache)
-		HIP_TRY(rtamd::launch_stream_read(b.p[1], bytes, 16, static_cast<unsigned long long*>(b.p[2]), nullptr));
-		HIP_TRY(rtamd::launch_stream_read(b.p[0], bytes, w, static_cast<unsigned long long*>(b.p[2]), nullptr));
-		HIP_TRY(hipDeviceSynchronize());
-	}
-	return RT_OK;
-}
-
-// Diagnostic (not in rtamd.h): VALU issue calibration.  k_valu_peak dispatches for each
-// instruction kind (v_fma_f32, v_pk_fma_f32, v_fma_f64) at 1, 2, 4 and 8 waves per SIMD
-// (each after a warm-up at the same shape), iterations scaled so that every dispatch issues
-// the same instructions per SIMD; profiled with rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU
-// SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE ..., they give cycles per wave64 instruction and the
-// shader clock (tools/valu_calibration.py, tools/make_valu.py).
-int rt_debug_valu_calibration(int device, int iters) {
-	HIP_TRY(hipSetDevice(device));
-	struct Sink {
-		void* p = nullptr;
-		~Sink() {
-			if (p) (void)dev_free(p);
-		}
-	} sink;
-	HIP_TRY(dev_alloc(&sink.p, 64));
-	for (int kind = 0; kind < 3; kind++)
-		for (int w = 1; w <= 8; w *= 2) {
-			const int it = std::max(1, iters * 8 / w);
-			HIP_TRY(rtamd::launch_valu_peak(std::max(1, it / 8), kind, w, sink.p, nullptr));  // warm-up (clocks)
-			HIP_TRY(rtamd::launch_valu_peak(it, kind, w, sink.p, nullptr));
-		}
-	HIP_TRY(hipDeviceSynchronize());
-	return RT_OK;
-}
-
-// Diagnostic (not in rtamd.h): k_valu_peak of one instruction kind (trace.hip kValuKinds) at
-// `waves` waves per SIMD, timed with events after a warm-up launch; *ms = kernel time.  The
-// kernel issues 256 * waves * 4 waves * iters * 128 instructions.
-int rt_debug_valu_rate(int device, int kind, int waves, int iters, double* ms) {
-	if (!ms || kind < 0 || waves < 1 || waves > 8 || iters < 1) return fail(RT_ERR_ARG, "bad calibration arguments");
-	HIP_TRY(hipSetDevice(device));
-	struct Res {
-		void* p = nullptr;
-		hipEvent_t e0 = nullptr, e1 = nullptr;
-		~Res() {
-			if (p) (void)dev_free(p);
-			if (e0) (void)hipEventDestroy(e0);
-			if (e1) (void)hipEventDestroy(e1);
-		}
-	} r;
-	HIP_TRY(dev_alloc(&r.p, 64));
-	HIP_TRY(hipEventCreate(&r.e0));
-	HIP_TRY(hipEventCreate(&r.e1));
-	HIP_TRY(rtamd::launch_valu_peak(std::max(1, iters / 4), kind, waves, r.p, nullptr));  // warm-up (clocks)
-	HIP_TRY(hipEventRecord(r.e0, nullptr));
-	HIP_TRY(rtamd::launch_valu_peak(iters, kind, waves, r.p, nullptr));
-	HIP_TRY(hipEventRecord(r.e1, nullptr));
-	HIP_TRY(hipEventSynchronize(r.e1));
-	float f = 0;
-	HIP_TRY(hipEventElapsedTime(&f, r.e0, r.e1));
-	*ms = f;
-	return RT_OK;
-}
-
-// Diagnostic (not in rtamd.h): the scene's next render fails after `launches` more
-// closest-hit launches, as a device failure in the middle of a render would (tests of the
-// error path: the render after it must be complete and exact).  -1 disables.
-int rt_debug_fail_after(rt_scene* s, int launches) {
-	if (!s) return fail(RT_ERR_ARG, "null scene");
-	s->fail_after = launches;
 	return RT_OK;
 }
 

@@ -50,24 +50,39 @@ struct RayLevel {
 	int32_t *child_refr, *child_refl;
 	int32_t* counts;             // [0] hits of this level (k_closest), [1] children spawned
 	int64_t capacity;
+	// level_tag(level): set by the host with the buffers; the kernels that read a record from
+	// the device copy check it (a record that is not the one uploaded raises DERR_RECORD and
+	// nothing is read through its pointers)
+	uint32_t tag;
+	uint32_t pad;
 };
+__host__ __device__ inline uint32_t level_tag(int level) { return 0x52544c00u ^ static_cast<uint32_t>(level); }
 
-// One row of a chunk: the image row it renders and where its pixels go.  A chunk holds
-// the selected rows of one frame or of several frames of the same width, height and depth
-// (rt_render_batch_device): small row selections, such as one GPU's share of
-// row-partitioned frames, are then traced as one full-size wavefront.
-struct ChunkRow {
-	int32_t row;       // image row r: Camera::calculateViewingRay's rowFrac = (r + 0.5) / H (scene.cpp:28)
-	int32_t pad;
-	double* out;       // this row's f64 pixels (W x 3), or null
-	uint8_t* out8;     // this row's RGB8 pixels, or null
+// A chunk holds the selected rows of one frame or of several frames of the same width,
+// height and depth (rt_render_batch_device): small row selections, such as one GPU's share
+// of row-partitioned frames, are then traced as one full-size wavefront.  Its rows are
+// described by value, in the kernel arguments: a segment is a run of rows of one job, whose
+// image rows and output rows follow from the ordinal arithmetically (scene.cpp:25-31: pixel
+// -> (r, c) -> output(r, c)), so no kernel reads a row table from memory.
+// Chunks are cut so that they never hold more segments than this (api.cpp plan_chunks).
+constexpr int kMaxRowSegments = 32;
+struct RowSegment {
+	double* out;          // the job's f64 rows: ordinal o at out + o * width * 3 (or null)
+	uint8_t* out8;        // its RGB8 rows, the same layout (or null)
+	int32_t q0;           // the chunk row of the segment's first row
+	int32_t ord0;         // that row's ordinal in the job's row selection
+	int32_t ord_end;      // the job's selected rows (ordinals at or past it: a corrupt descriptor)
+	int32_t row_begin;    // image row of ordinal o: row_begin + (o / row_block) * row_span + o % row_block
+	int32_t row_block;    // (rt_render_params: row_block >= 1, row_span = row_step * row_block;
+	int32_t row_span;     //  the image row r gives rowFrac = (r + 0.5) / H, scene.cpp:28)
 };
-
 struct FrameGeometry {
 	int32_t width, height;
 	int32_t intersection_only;
+	int32_t n_rows;       // rows of the chunk: pixel i is column i % width of chunk row i / width
+	int32_t n_segs;       // 1 .. kMaxRowSegments, seg[k].q0 ascending from seg[0].q0 = 0
 	int32_t pad;
-	const ChunkRow* rows;         // the chunk's rows (device), pixel i -> row i / width
+	RowSegment seg[kMaxRowSegments];
 };
 
 // Row partition over devices (rt_partition_row): blocks of B rows interleaved over n
@@ -155,8 +170,8 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 // ShadeBatch::fused may be set only when this holds (the wave-packet all-lights form; with
 // per_lane also the per-lane one of scenes without LBVHs)
 bool shadow_can_fuse(const DeviceScene& s, const ShadeBatch& b, int packet_mask, bool per_lane);
-hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
-                        DeviceCounters* ctr, hipStream_t stream);
+hipError_t launch_shade(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
+                        hipStream_t stream);
 // n: the level's ray count, or with n_dev (the previous level's child counter) read on the
 // device (a fixed grid strides over it)
 hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,
@@ -173,7 +188,7 @@ struct FusedOut {
 	uint32_t* done;
 };
 // lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output;
-// pixels go to their rows' outputs (fg.rows); finish non-null: the statistics finish too
+// pixels go to their rows' outputs (fg.seg); finish non-null: the statistics finish too
 hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
                          unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr = nullptr,
                          const FusedOut* finish = nullptr);
@@ -199,8 +214,6 @@ hipError_t read_phase_profile(unsigned long long* out /* 4 * kPhaseSlots */);
 // RT_DIAG_WAVETIME builds: the wave records since the last call (32 B each, intersect.h
 // WaveTime), at most max_records, then cleared; 0 in other builds, -1 on a HIP error
 int read_wave_times(void* out, int max_records);
-// every XCD's L2 and the CUs' L1s drop their non-coherent lines (system-scope acquire)
-hipError_t launch_invalidate_caches(hipStream_t stream);
 // FETCH_SIZE calibration: reads `bytes` of buf once, `width` (1, 4, 8, 16) bytes per lane
 // VALU issue calibration: kind 0 v_fma_f32, 1 v_pk_fma_f32, 2 v_fma_f64 chains at
 // waves_per_simd waves on every SIMD

@@ -97,14 +97,45 @@ __device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, i
 	d = normalized3(dv);
 }
 
+// Chunk row q (FrameGeometry): its segment k, the last one starting at or before q (a loop
+// over the by-value descriptors with a wave-uniform bound: scalar loads of the kernel
+// arguments), the job's row ordinal and the image row, computed as the host's
+// selected_row (api.cpp).  False when the descriptor names no selected row of the frame
+// (corrupt): the caller raises DERR_ROWS and writes nothing for it.
+struct ChunkRowRef {
+	int32_t k, ord, row;
+};
+// (The descriptors are read through an opaque pointer where they are used, so that the
+// compiler does not hoist them out of the grid-stride loops into scalar registers held
+// through the traversals.)
+__device__ __forceinline__ bool chunk_row(const FrameGeometry& fg0, int64_t q, ChunkRowRef& r) {
+	const auto* fg = uniform_ptr(opaque(&fg0));
+	int k = 0;
+	for (int j = 1; j < fg->n_segs; j++) k = q >= fg->seg[j].q0 ? j : k;
+	const auto& sg = fg->seg[k];
+	const int64_t ord = sg.ord0 + (q - sg.q0);
+	const int64_t blk = sg.row_block >= 1 ? sg.row_block : 1;
+	const int64_t nb = div_small(ord >= 0 ? ord : 0, blk);
+	const int64_t row = sg.row_begin + nb * sg.row_span + (ord - nb * blk);
+	r.k = k;
+	r.ord = static_cast<int32_t>(ord);
+	r.row = static_cast<int32_t>(row);
+	return q >= 0 && q < fg->n_rows && ord >= 0 && ord < sg.ord_end && sg.row_block >= 1 && row >= 0 &&
+	       row < fg->height;
+}
+
 template <typename LV>
 __device__ __forceinline__ void level_ray(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t i,
                                           const LV& cur, V3& o, V3& d, bool& inside, DeviceCounters* ctr) {
 	if (level == 0) {
 		const int64_t q = div_small(i, fg.width);
-		const int r = fg.rows[q].row;
+		ChunkRowRef rr;
+		if (!chunk_row(fg, q, rr)) {
+			raise_error(ctr, DERR_ROWS);
+			rr.row = 0;  // a ray of a valid row: its pixel is never written (write_pixel checks again)
+		}
 		const int c = (int)(i - q * fg.width);
-		primary_ray(S.cam, r, c, fg.width, fg.height, o, d, ctr);
+		primary_ray(S.cam, rr.row, c, fg.width, fg.height, o, d, ctr);
 		inside = false;
 	} else {
 		o = mk(cur.ox[i], cur.oy[i], cur.oz[i]);
@@ -254,22 +285,40 @@ __device__ __forceinline__ uint8_t to_u8(double v) {
 	return (v == v) ? (uint8_t)(int)v : (uint8_t)0;
 }
 
-// pixel i of the chunk (column c of its row q) into that row's outputs: f64 and RGB8
-__device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, const double v[3], bool rgb8) {
+// pixel i of the chunk (column c of its row q) into that row's outputs: f64 and RGB8, at
+// the job's row ordinal (a descriptor that names no selected row writes nothing)
+__device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, const double v[3], bool rgb8,
+                                            DeviceCounters* ctr) {
 	const int64_t q = div_small(i, fg.width);
 	const int64_t c = i - q * fg.width;
-	double* out = fg.rows[q].out;
-	uint8_t* out8 = fg.rows[q].out8;
+	ChunkRowRef rr;
+	if (!chunk_row(fg, q, rr)) {
+		raise_error(ctr, DERR_ROWS);
+		return;
+	}
+	const auto& sg = uniform_ptr(opaque(&fg))->seg[rr.k];
+	const int64_t at = (static_cast<int64_t>(rr.ord) * fg.width + c) * 3;
+	double* out = sg.out;
+	uint8_t* out8 = sg.out8;
 	if (out) {
-		out[c * 3 + 0] = v[0];
-		out[c * 3 + 1] = v[1];
-		out[c * 3 + 2] = v[2];
+		out[at + 0] = v[0];
+		out[at + 1] = v[1];
+		out[at + 2] = v[2];
 	}
 	if (out8 && rgb8) {
-		out8[c * 3 + 0] = to_u8(v[0]);
-		out8[c * 3 + 1] = to_u8(v[1]);
-		out8[c * 3 + 2] = to_u8(v[2]);
+		out8[at + 0] = to_u8(v[0]);
+		out8[at + 1] = to_u8(v[1]);
+		out8[at + 2] = to_u8(v[2]);
 	}
+}
+
+// The level records a launch reads from the device copy carry their tag (RayLevel::tag): a
+// record that is not the uploaded one raises DERR_RECORD and the block leaves before any
+// pointer of it is used (block-uniform: every thread reads the same records)
+__device__ __forceinline__ bool record_ok(const RayLevel* levels, int level, DeviceCounters* ctr) {
+	const bool ok = uniform_ptr(levels)[level].tag == level_tag(level);
+	if (!ok && threadIdx.x == 0) raise_error(ctr, DERR_RECORD);
+	return ok;
 }
 
 template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
@@ -444,7 +493,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 		}
 		if (!active) return;
 		if (fo->final) {
-			write_pixel(fg, i, col, true);
+			write_pixel(fg, i, col, true, ctr);
 		} else {
 			cur.cr[i] = col[0];
 			cur.cg[i] = col[1];
@@ -487,6 +536,7 @@ __global__ void __launch_bounds__(kBlock)
 	// the traversal stacks (LBVH searches: none in a scene of spheres only)
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
+	if (!record_ok(levels, level, ctr) || (remaining > 0 && !record_ok(levels, level + 1, ctr))) return;
 	// level records read through the constant address space (scalar loads at their uses)
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -594,6 +644,7 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ double park_mem[RT_FUSED_PARK && kPacket ? 6 * kBlock : 1];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
+	if (!record_ok(levels, level, ctr) || (remaining > 0 && !record_ok(levels, level + 1, ctr))) return;
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
 	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur0.capacity) : n_host;
@@ -873,6 +924,8 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
+	for (int k = 0; k < B.n; k++)
+		if (!record_ok(levels, B.level[k], ctr)) return;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride) {
@@ -883,8 +936,10 @@ __global__ void __launch_bounds__(kBlock)
 }
 
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
-__global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, FrameGeometry fg, ShadeBatch B,
-                                                       const RayLevel* levels, DeviceCounters* ctr) {
+__global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, ShadeBatch B, const RayLevel* levels,
+                                                       DeviceCounters* ctr) {
+	for (int k = 0; k < B.n; k++)
+		if (!record_ok(levels, B.level[k], ctr)) return;
 	// glibc pow tables in LDS: the specular pow's two dependent table lookups per light
 	// are LDS latency instead of divergent L2 gathers
 	__shared__ double log_tab[512];
@@ -955,7 +1010,7 @@ __global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lv
 			v[1] = lvl0.cg[i];
 			v[2] = lvl0.cb[i];
 		}
-		write_pixel(fg, i, v, !io);
+		write_pixel(fg, i, v, !io, ctr);
 	}
 	if (io) {  // running max of maxCoeff over positive doubles (bit order == value order)
 		const double m = (i < n) ? fmax(fmax(v[0], v[1]), v[2]) : 0.0;
@@ -1249,12 +1304,12 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 	return hipGetLastError();
 }
 
-hipError_t launch_shade(const DeviceScene& s, const FrameGeometry& fg, const ShadeBatch& b, const RayLevel* levels_dev,
-                        DeviceCounters* ctr, hipStream_t stream) {
+hipError_t launch_shade(const DeviceScene& s, const ShadeBatch& b, const RayLevel* levels_dev, DeviceCounters* ctr,
+                        hipStream_t stream) {
 	const int64_t items = b.shade_begin[b.n];  // device-counted: an upper bound
 	if (items <= 0) return hipSuccess;
 	const unsigned grid = b.dev_counts ? dev_grid(items, kShadeBlock) : grid_for(items, kShadeBlock);
-	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, fg, b, levels_dev, ctr);
+	hipLaunchKernelGGL(k_shade, dim3(grid), dim3(kShadeBlock), 0, stream, s, b, levels_dev, ctr);
 	return hipGetLastError();
 }
 
@@ -1332,17 +1387,6 @@ hipError_t read_phase_profile(unsigned long long* out) {
 	for (int k = 0; k < 4 * kPhaseSlots; k++) out[k] = 0;
 	return hipSuccess;
 #endif
-}
-
-// A system-scope acquire on every XCD (buffer_inv sc0 sc1: the CU's L1 and its XCD's L2 drop
-// their non-coherent lines): 2048 blocks, dealt round-robin over the XCDs and their CUs
-__global__ void k_invalidate_caches() {
-	__builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-	asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-hipError_t launch_invalidate_caches(hipStream_t stream) {
-	hipLaunchKernelGGL(k_invalidate_caches, dim3(2048), dim3(64), 0, stream);  // every CU, every XCD
-	return hipGetLastError();
 }
 
 int read_wave_times(void* out, int max_records) {

@@ -24,6 +24,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # RTAMD_LIB: an alternative build of the same library (e.g. the phase-profile build, make prof)
 LIB_PATH = os.environ.get("RTAMD_LIB") or os.path.join(_HERE, "librtamd.so")
+# the same library with the test and measurement hooks (csrc/diag.cpp: rt_debug_*, not in
+# rtamd.h): only tests that inject failures and the profiling tools load it
+DIAG_LIB_PATH = os.path.join(_HERE, "librtamd_diag.so")
 
 RT_OK, RT_ERR_PARSE, RT_ERR_MATH, RT_ERR_ARG, RT_ERR_DEVICE, RT_ERR_IO = 0, -1, -2, -3, -4, -5
 
@@ -128,17 +131,19 @@ RT_LIGHT_POINT, RT_LIGHT_DIRECTIONAL, RT_LIGHT_AMBIENT = 0, 1, 2
 
 PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_int, ctypes.c_void_p)
 
-_lib: Optional[ctypes.CDLL] = None
+_libs: dict = {}
 RTAMD_ABI_VERSION = 5  # include/rtamd.h
 
 
-def lib() -> ctypes.CDLL:
-    """Loads librtamd.so (built in-tree by ``make -C cs184-raytracer_amd``); fails loudly."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"{LIB_PATH} is missing: build it with `make -C cs184-raytracer_amd` "
+def lib(diag: bool = False) -> ctypes.CDLL:
+    """Loads librtamd.so (built in-tree by ``make -C cs184-raytracer_amd``); fails loudly.
+    ``diag``: librtamd_diag.so instead, the same library with the rt_debug_* hooks (a separate
+    instance: its scenes are its own)."""
+    path = DIAG_LIB_PATH if diag else LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
+        raise ImportError(f"{path} is missing: build it with `make -C cs184-raytracer_amd` "
                           "(or __graft_entry__.build())")
     try:
         # One HIP runtime per process: when PyTorch is present its libamdhip64.so.7 must be
@@ -146,7 +151,7 @@ def lib() -> ctypes.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, cp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
     sig = {
         "rt_builder_create": (vp, []),
@@ -164,8 +169,6 @@ def lib() -> ctypes.CDLL:
         "rt_builder_get_desc": (i32, [vp, ctypes.POINTER(rt_scene_desc)]),
         "rt_builder_set_desc": (i32, [vp, ctypes.POINTER(rt_scene_desc)]),
         "rt_scene_create_desc": (i32, [ctypes.POINTER(rt_scene_desc), i32, ctypes.POINTER(vp)]),
-        "rt_debug_builder_digest": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
-        "rt_debug_fail_after": (i32, [vp, i32]),
         "rt_partition_row": (None, [i64, i32, i32, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int64)]),
         "rt_render_batch_device": (i32, [vp, i32, ctypes.POINTER(rt_render_params), ctypes.POINTER(vp),
                                          ctypes.POINTER(vp), vp, ctypes.POINTER(rt_counters)]),
@@ -177,6 +180,20 @@ def lib() -> ctypes.CDLL:
         "rt_device_count": (i32, []),
         "rt_selftest_math": (i32, [i32, i32, vp, vp, vp, i64]),
     }
+    if diag:
+        sig.update({
+            "rt_debug_builder_digest": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
+            "rt_debug_fail_after": (i32, [vp, i32]),
+            "rt_debug_corrupt_rows": (i32, [vp]),
+            "rt_debug_corrupt_level_record": (i32, [vp, i32, i32]),
+            "rt_debug_plan_chunks": (i32, [i32, ctypes.POINTER(rt_render_params), i32, i64, i32,
+                                           ctypes.POINTER(ctypes.c_int64), i32]),
+            "rt_debug_phase_profile": (i32, [i32, vp]),
+            "rt_debug_wave_times": (i32, [i32, vp, i32]),
+            "rt_debug_fetch_calibration": (i32, [i32, i64]),
+            "rt_debug_valu_calibration": (i32, [i32, i32]),
+            "rt_debug_valu_rate": (i32, [i32, i32, i32, i32, ctypes.POINTER(dbl)]),
+        })
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
         fn.restype = res
@@ -184,13 +201,13 @@ def lib() -> ctypes.CDLL:
     # the ctypes structs above mirror include/rtamd.h of this ABI version (RTAMD_ABI_CHECK=0
     # loads a library of an older revision for a bisection: its structs must be a prefix of these)
     if os.environ.get("RTAMD_ABI_CHECK") == "0" and not hasattr(L, "rt_abi_version"):
-        _lib = L
+        _libs[path] = L
         return L
     L.rt_abi_version.restype, L.rt_abi_version.argtypes = i32, []
     if L.rt_abi_version() != RTAMD_ABI_VERSION:
-        raise ImportError(f"{LIB_PATH} has ABI version {L.rt_abi_version()}, this binding expects "
+        raise ImportError(f"{path} has ABI version {L.rt_abi_version()}, this binding expects "
                           f"{RTAMD_ABI_VERSION} (include/rtamd.h RTAMD_ABI_VERSION): rebuild it")
-    _lib = L
+    _libs[path] = L
     return L
 
 
@@ -212,10 +229,10 @@ def selected_count(begin: int, end: int, step: int, block: int = 1) -> int:
     return len(selected_rows(begin, end, step, block))
 
 
-def _raise(rc: int, what: str = "") -> None:
+def _raise(rc: int, what: str = "", L: Optional[ctypes.CDLL] = None) -> None:
     if rc == RT_OK:
         return
-    msg = lib().rt_last_error().decode(errors="replace")
+    msg = (L or lib()).rt_last_error().decode(errors="replace")
     cls = {RT_ERR_PARSE: ParseException, RT_ERR_MATH: MathException, RT_ERR_ARG: ArgumentError,
            RT_ERR_DEVICE: DeviceError, RT_ERR_IO: WriteException}.get(rc, RTError)
     raise cls(msg or what)
@@ -279,8 +296,10 @@ def _stats(c: rt_counters) -> RenderStats:
 class Scene:
     """Scene (scene.h:9-39): accumulates parsed files; uploads to HBM on first render."""
 
-    def __init__(self, device: int = 0):
-        self._b = lib().rt_builder_create()
+    def __init__(self, device: int = 0, diag: bool = False):
+        """``diag``: the scene lives in librtamd_diag.so (test hooks: digest, debug_*)."""
+        self._L = lib(diag)
+        self._b = self._L.rt_builder_create()
         self._scene = None
         self.device = device
         self.last_stats: Optional[RenderStats] = None
@@ -293,29 +312,29 @@ class Scene:
 
     def close(self) -> None:
         if getattr(self, "_scene", None):
-            lib().rt_scene_destroy(self._scene)
+            self._L.rt_scene_destroy(self._scene)
             self._scene = None
         if getattr(self, "_b", None):
-            lib().rt_builder_destroy(self._b)
+            self._L.rt_builder_destroy(self._b)
             self._b = None
 
     def hasCamera(self) -> bool:  # scene.h:20
-        return bool(lib().rt_builder_has_camera(self._b))
+        return bool(self._L.rt_builder_has_camera(self._b))
 
     def warnings(self) -> str:
-        return lib().rt_builder_warnings(self._b).decode()
+        return self._L.rt_builder_warnings(self._b).decode()
 
     def _parse(self, filename: str) -> None:
         if self._scene:
             raise ArgumentError("scene already uploaded; parse all files before rendering")
-        _raise(lib().rt_builder_parse_rti(self._b, os.fsencode(filename)))
+        _raise(self._L.rt_builder_parse_rti(self._b, os.fsencode(filename)), L=self._L)
 
     def upload(self) -> None:
         """rt_scene_create: build the LBVHs and upload the scene to the device once."""
         if self._scene:
             return
         p = ctypes.c_void_p()
-        _raise(lib().rt_scene_create(self._b, self.device, ctypes.byref(p)))
+        _raise(self._L.rt_scene_create(self._b, self.device, ctypes.byref(p)), L=self._L)
         self._scene = p
 
     @property
@@ -325,7 +344,7 @@ class Scene:
 
     def info(self) -> rt_scene_info:
         i = rt_scene_info()
-        _raise(lib().rt_scene_get_info(self.handle, ctypes.byref(i)))
+        _raise(self._L.rt_scene_get_info(self.handle, ctypes.byref(i)), L=self._L)
         return i
 
     def params(self, width: int, height: int, bounce_depth: int, intersection_only: bool, row_begin: int = 0,
@@ -357,8 +376,8 @@ class Scene:
         prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels, blk)
         cb = PROGRESS_FN((lambda c, t, u: phandler(c, t)) if phandler else (lambda c, t, u: None))
         cnt = rt_counters()
-        _raise(lib().rt_render(self.handle, ctypes.byref(prm), output.ctypes.data_as(ctypes.c_void_p), cb, None,
-                               ctypes.byref(cnt)))
+        _raise(self._L.rt_render(self.handle, ctypes.byref(prm), output.ctypes.data_as(ctypes.c_void_p), cb, None,
+                               ctypes.byref(cnt)), L=self._L)
         self.last_stats = _stats(cnt)
         return output
 
@@ -374,8 +393,8 @@ class Scene:
         prm = self.params(W, H, o.bounceDepth_, o.intersectionOnly_, rb, re_, rs, chunk_pixels, blk)
         cb = PROGRESS_FN((lambda c, t, u: phandler(c, t)) if phandler else (lambda c, t, u: None))
         cnt = rt_counters()
-        _raise(lib().rt_render_rgb8(self.handle, ctypes.byref(prm), out.ctypes.data_as(ctypes.c_void_p), cb, None,
-                                    ctypes.byref(cnt)))
+        _raise(self._L.rt_render_rgb8(self.handle, ctypes.byref(prm), out.ctypes.data_as(ctypes.c_void_p), cb, None,
+                                    ctypes.byref(cnt)), L=self._L)
         self.last_stats = _stats(cnt)
         return out
 
@@ -383,40 +402,52 @@ class Scene:
         """rt_builder_get_desc: the parsed scene as a flat descriptor (views into the builder,
         valid while this Scene lives and parses nothing more)."""
         d = rt_scene_desc()
-        _raise(lib().rt_builder_get_desc(self._b, ctypes.byref(d)))
+        _raise(self._L.rt_builder_get_desc(self._b, ctypes.byref(d)), L=self._L)
         return d
 
     def set_desc(self, d: rt_scene_desc) -> None:
         """rt_builder_set_desc: replace the (not yet uploaded) scene by a descriptor's."""
         if self._scene:
             raise ArgumentError("scene already uploaded")
-        _raise(lib().rt_builder_set_desc(self._b, ctypes.byref(d)))
+        _raise(self._L.rt_builder_set_desc(self._b, ctypes.byref(d)), L=self._L)
 
     @classmethod
-    def from_desc(cls, d: rt_scene_desc, device: int = 0) -> "Scene":
+    def from_desc(cls, d: rt_scene_desc, device: int = 0, diag: bool = False) -> "Scene":
         """rt_scene_create_desc: a device scene straight from a descriptor (no builder scene)."""
-        s = cls(device)
+        s = cls(device, diag)
         p = ctypes.c_void_p()
-        _raise(lib().rt_scene_create_desc(ctypes.byref(d), device, ctypes.byref(p)))
+        _raise(s._L.rt_scene_create_desc(ctypes.byref(d), device, ctypes.byref(p)), L=s._L)
         s._scene = p
         return s
 
     def digest(self) -> int:
-        """Host-side digest of the device scene rt_scene_create would upload (diagnostic)."""
+        """Host-side digest of the device scene rt_scene_create would upload (diag scenes)."""
         h = ctypes.c_uint64()
-        _raise(lib().rt_debug_builder_digest(self._b, ctypes.byref(h)))
+        _raise(self._L.rt_debug_builder_digest(self._b, ctypes.byref(h)), L=self._L)
         return h.value
 
     def debug_fail_after(self, launches: int) -> None:
-        """Fault injection: the next render fails after `launches` closest-hit launches."""
-        _raise(lib().rt_debug_fail_after(self.handle, launches))
+        """Fault injection (diag scenes): the next render fails after `launches` closest-hit launches."""
+        _raise(self._L.rt_debug_fail_after(self.handle, launches), L=self._L)
+
+    def debug_corrupt_rows(self) -> None:
+        """Fault injection (diag scenes): the next chunk's row descriptors name rows no frame has."""
+        _raise(self._L.rt_debug_corrupt_rows(self.handle), L=self._L)
+
+    def debug_corrupt_level_record(self, lane: int, level: int) -> bool:
+        """Fault injection (diag scenes): zeroes the device copy of a lane's level record (an
+        upload that never arrived); False when that lane or level does not exist."""
+        rc = self._L.rt_debug_corrupt_level_record(self.handle, lane, level)
+        if rc < 0:
+            _raise(rc, L=self._L)
+        return rc == 0
 
     def render_device(self, params: rt_render_params, out_rgb_ptr: int = 0, out_rgb8_ptr: int = 0,
                       stream_ptr: int = 0) -> RenderStats:
         """rt_render_device into device buffers (e.g. torch tensors' data_ptr())."""
         cnt = rt_counters()
-        _raise(lib().rt_render_device(self.handle, ctypes.byref(params), out_rgb_ptr or None, out_rgb8_ptr or None,
-                                      stream_ptr or None, ctypes.byref(cnt)))
+        _raise(self._L.rt_render_device(self.handle, ctypes.byref(params), out_rgb_ptr or None, out_rgb8_ptr or None,
+                                      stream_ptr or None, ctypes.byref(cnt)), L=self._L)
         self.last_stats = _stats(cnt)
         return self.last_stats
 
@@ -428,15 +459,15 @@ class Scene:
         prm = (rt_render_params * max(n, 1))(*params)
         ptrs = lambda xs: (ctypes.c_void_p * max(n, 1))(*[(xs[k] if k < len(xs) else 0) or None for k in range(n)])
         cnt = rt_counters()
-        _raise(lib().rt_render_batch_device(self.handle, n, prm, ptrs(out_rgb_ptrs), ptrs(out_rgb8_ptrs),
-                                            stream_ptr or None, ctypes.byref(cnt)))
+        _raise(self._L.rt_render_batch_device(self.handle, n, prm, ptrs(out_rgb_ptrs), ptrs(out_rgb8_ptrs),
+                                            stream_ptr or None, ctypes.byref(cnt)), L=self._L)
         self.last_stats = _stats(cnt)
         return self.last_stats
 
     def normalize_device(self, rgb_ptr: int, n_pixels: int, max_value: float, out_rgb8_ptr: int = 0,
                          stream_ptr: int = 0) -> None:
-        _raise(lib().rt_normalize_device(self.handle, rgb_ptr, n_pixels, max_value, out_rgb8_ptr or None,
-                                         stream_ptr or None))
+        _raise(self._L.rt_normalize_device(self.handle, rgb_ptr, n_pixels, max_value, out_rgb8_ptr or None,
+                                         stream_ptr or None), L=self._L)
 
 
 class RTIParser:
@@ -493,9 +524,9 @@ def selftest_math(op: str, x: np.ndarray, y: Optional[np.ndarray] = None, device
     return out
 
 
-def load_scene(files, device: int = 0) -> Scene:
-    """main.cpp:53-66: one RTIParser per file, camera required."""
-    s = Scene(device)
+def load_scene(files, device: int = 0, diag: bool = False) -> Scene:
+    """main.cpp:53-66: one RTIParser per file, camera required (``diag``: in librtamd_diag.so)."""
+    s = Scene(device, diag)
     for f in ([files] if isinstance(files, (str, os.PathLike)) else files):
         RTIParser(s).parseFile(str(f))
     if not s.hasCamera():

@@ -237,10 +237,8 @@ int rt_render_rgb8(rt_scene* s, const rt_render_params* p, uint8_t* out_rgb8,
 
 /* Same, with outputs in device memory (either may be NULL): out_rgb_dev (n_rows*W*3
  * doubles) and out_rgb8_dev (n_rows*W*3 bytes, writers.cpp:4-9 quantisation fused).
- * `stream` is a hipStream_t; NULL = the scene's own non-blocking stream (the default).
- * Opt-in exceptions: RTAMD_SCENE_STREAM=0 makes that stream at the scene's second call (the
- * null stream until then), =2 always uses the null stream.  The call returns when the work
- * on the stream is complete. */
+ * `stream` is a hipStream_t; NULL = the scene's own non-blocking stream.  The call returns
+ * when the work on the stream is complete. */
 int rt_render_device(rt_scene* s, const rt_render_params* p, double* out_rgb_dev,
                      uint8_t* out_rgb8_dev, void* stream, rt_counters* counters);
 

@@ -138,7 +138,7 @@ def test_render_after_a_failed_render_is_exact(gpu, oracle, after, replay):
     scene = "excess_inputs/bunny.rti"
     w, h, bdepth = 80, 45, 4
     want, cnt = oracle.render(os.path.join(SCENES, scene), w, h, bdepth=bdepth)
-    s = gpu.load_scene(os.path.join(SCENES, scene))
+    s = gpu.load_scene(os.path.join(SCENES, scene), diag=True)
     o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth)
     # lanes and level buffers exist; with replay, a plan of this shape too
     s.renderScene(options=o if replay else gpu.Options(renderWidth_=w + 8, renderHeight_=h, bounceDepth_=bdepth))
@@ -148,6 +148,100 @@ def test_render_after_a_failed_render_is_exact(gpu, oracle, after, replay):
     img = s.renderScene(options=o)
     assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
     assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+    s.close()
+
+
+@pytest.mark.parametrize("replay", [True, False])
+def test_corrupt_row_descriptor_is_reported_not_written(gpu, oracle, replay):
+    """The kernels compute every row and output address from by-value descriptors and check
+    them (trace.hip chunk_row): descriptors naming rows the frame does not have (injected,
+    librtamd_diag.so) fail the render with the named device error, write no pixel, and the
+    scene's next render is exact."""
+    torch = pytest.importorskip("torch")
+    scene = os.path.join(SCENES, "excess_inputs/bunny.rti")
+    w, h, bdepth = 64, 40, 4
+    want, _ = oracle.render(scene, w, h, bdepth=bdepth)
+    s = gpu.load_scene(scene, diag=True)
+    prm = s.params(w, h, bdepth, False)
+    out = torch.full((h, w, 3), -7.0, dtype=torch.float64, device="cuda")
+    if replay:  # a launch plan of this shape exists: the bad chunk replays it on the caller's stream
+        s.render_device(prm, out.data_ptr())
+        out.fill_(-7.0)
+    s.debug_corrupt_rows()
+    with pytest.raises(gpu.DeviceError, match="row descriptor names no selected row"):
+        s.render_device(prm, out.data_ptr())
+    # segment 0's rows moved past the image: nothing written
+    assert bool((out == -7.0).all())
+    s.render_device(prm, out.data_ptr())
+    assert np.array_equal(out.cpu().numpy().view(np.uint64), want.view(np.uint64))
+    s.close()
+
+
+@pytest.mark.parametrize("level", [0, 1, 3])
+def test_missing_level_record_is_reported_not_read(gpu, oracle, level):
+    """A device level record that does not hold its upload (the form of the round-5
+    multi-process failures; injected here by zeroing it, librtamd_diag.so) is caught by its
+    tag (RayLevel::tag): the render fails with the named device error instead of following
+    its pointers, and the next render, after the records are uploaded again, is exact."""
+    scene = os.path.join(SCENES, "excess_inputs/bunny.rti")
+    w, h, bdepth = 64, 40, 4
+    want, cnt = oracle.render(scene, w, h, bdepth=bdepth)
+    s = gpu.load_scene(scene, diag=True)
+    o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth)
+    s.renderScene(options=o)
+    s.renderScene(options=o)  # the second call has lane streams and a plan; the third replays it
+    assert s.debug_corrupt_level_record(0, level)
+    with pytest.raises(gpu.DeviceError, match="level record"):
+        s.renderScene(options=o)
+    img = s.renderScene(options=o)
+    assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
+    assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
+    s.close()
+
+
+def test_right_sized_levels_then_replay_on_a_torch_stream(gpu, oracle):
+    """a call traced host-driven grows the level buffers and cuts them back after it
+    (right_size_levels, record copies on the lane's stream); the next call of that shape replays
+    its plan on the caller's stream.  The record copies complete before the first call returns,
+    so the replay on a torch stream reads the new records: exact, three times."""
+    torch = pytest.importorskip("torch")
+    scene = os.path.join(SCENES, "excess_inputs/bunny.rti")
+    w, h, bdepth = 480, 270, 4
+    want, _ = oracle.render(scene, w, h, bdepth=bdepth)
+    s = gpu.load_scene(scene)
+    prm = s.params(w, h, bdepth, False)
+    st = torch.cuda.Stream()
+    out = torch.empty((h, w, 3), dtype=torch.float64, device="cuda")
+    s.renderScene(options=gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth))  # minimal lane
+    for _ in range(3):
+        with torch.cuda.stream(st):
+            out.fill_(0.0)
+            s.render_device(prm, out.data_ptr(), 0, st.cuda_stream)
+        st.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint64), want.view(np.uint64))
+    assert s.info().level_bytes <= s.info().level_bytes_peak
+    s.close()
+
+
+def test_chunks_of_many_row_segments(gpu, oracle, monkeypatch):
+    """More jobs of a few rows than one chunk's by-value descriptors hold (kMaxRowSegments):
+    the chunks are cut at 32 segments, and every job's rows land in its own buffer, exact."""
+    torch = pytest.importorskip("torch")
+    scene = os.path.join(SCENES, "inputs/input-06.rti")
+    w, h, bdepth = 48, 80, 3
+    want, _ = oracle.render(scene, w, h, bdepth=bdepth)
+    s = gpu.load_scene(scene)
+    ways = 10  # 10 ranks' 8-row blocks of 8 frames: 80 jobs of 8 rows
+    jobs, rows = [], []
+    for f in range(8):
+        for k in range(ways):
+            jobs.append(s.params(w, h, bdepth, False, ((k + f) % ways) * 8, h, ways, row_block=8))
+            rows.append([r for r in range(h) if (r // 8) % ways == (k + f) % ways])
+    outs = [torch.full((len(r), w, 3), -1.0, dtype=torch.float64, device="cuda") for r in rows]
+    for _ in range(2):  # host-driven, then replayed plans
+        s.render_batch_device(jobs, [o.data_ptr() for o in outs], [0] * len(jobs))
+        for o, r in zip(outs, rows):
+            assert np.array_equal(o.cpu().numpy().view(np.uint64), np.ascontiguousarray(want[r]).view(np.uint64))
     s.close()
 
 

@@ -28,6 +28,24 @@ def test_library_exports_every_declared_function(rt):
         assert hasattr(rt.lib(), n), f"{n} declared in include/rtamd.h but not exported"
 
 
+DIAG_HOOKS = ["rt_debug_builder_digest", "rt_debug_fail_after", "rt_debug_corrupt_rows",
+              "rt_debug_corrupt_level_record", "rt_debug_plan_chunks", "rt_debug_phase_profile",
+              "rt_debug_wave_times", "rt_debug_fetch_calibration", "rt_debug_valu_calibration", "rt_debug_valu_rate"]
+
+
+def test_production_library_has_no_debug_hooks(rt):
+    """The test and measurement hooks live in librtamd_diag.so only (csrc/diag.cpp): the
+    product library exports the rtamd.h surface and nothing named rt_debug_*."""
+    names = subprocess.run(["nm", "-D", "--defined-only", rt.LIB_PATH], capture_output=True, text=True,
+                           check=True).stdout
+    assert "rt_debug_" not in names
+    diag = rt.lib(diag=True)
+    for n in DIAG_HOOKS:
+        assert hasattr(diag, n), n
+    for n in declared_functions():
+        assert hasattr(diag, n), n
+
+
 def test_multi_library_exports_every_declared_function(rt):
     """librtamd_multi.so (RCCL multi-GPU render) exports include/rtamd_multi.h; loading it
     needs no GPU."""
@@ -150,14 +168,10 @@ def test_libm_pow_identities_used_by_shading():
 def _plan(rt, params, lanes, chunk=1 << 22, balance=1):
     """rt_debug_plan_chunks: [(chunk, job, r0, rows)] of a render call (no device needed)."""
     import ctypes
-    L = rt.lib()
-    f = L.rt_debug_plan_chunks
-    f.restype = ctypes.c_int
-    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
-                  ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    f = rt.lib(diag=True).rt_debug_plan_chunks
     arr = (rt.rt_render_params * len(params))(*params)
     out = (ctypes.c_int64 * (4 * 100000))()
-    q = f(len(params), ctypes.cast(arr, ctypes.c_void_p), lanes, chunk, balance, out, 100000)
+    q = f(len(params), arr, lanes, chunk, balance, out, 100000)
     assert q >= 0
     return [tuple(out[4 * k:4 * k + 4]) for k in range(q)]
 

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(REPO, "cs184-raytracer_amd"))
 import rtamd  # noqa: E402
 
 BYTES = 1 << 30
-L = rtamd.lib()
+L = rtamd.lib(diag=True)
 L.rt_debug_fetch_calibration.restype = ctypes.c_int
 L.rt_debug_fetch_calibration.argtypes = [ctypes.c_int, ctypes.c_int64]
 rc = L.rt_debug_fetch_calibration(0, BYTES)

@@ -23,7 +23,7 @@ KINDS = ["v_fma_f32", "v_pk_fma_f32", "v_fma_f64", "v_add_f64", "v_mul_f64", "v_
          "v_sqrt_f64"]
 SIMDS, CLOCK_GHZ = 1024, 2.4
 
-L = rtamd.lib()
+L = rtamd.lib(diag=True)
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 iters = int(args[0]) if args else 2000
 if "--mix" in sys.argv:
