@@ -509,7 +509,9 @@ BATCH_FRAMES = {"C5_refraction3_4096_bd8": 16}  # frames per emulated batch step
 def emulated_batch_partition(a, s, W, H, kw, blk, cfg, torch, n=8):
     """The throughput form of an n-GPU node for a sweep config (VERDICT r4 "next" 3): every
     rank renders its row blocks of the SAME F frames in one rt_render_batch_device call (the
-    bench's partition mode), emulated on this one GPU one rank's share at a time; the node's
+    bench's partition mode: rotated, frame f's blocks of residue (rank + f) mod n, so that with
+    F a multiple of n every rank renders the same rows in total), emulated on this one GPU one
+    rank's share at a time; the node's
     step takes the slowest share or the assumed gather of its F x rows of RGB8, whichever is
     longer: the bench overlaps a step's gather with the next step's render (main(), side
     stream, double-buffered RGB8), so in steady state the two run concurrently; the serial
@@ -533,9 +535,11 @@ def emulated_batch_partition(a, s, W, H, kw, blk, cfg, torch, n=8):
 
     whole_ms, whole_rays = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)] * F, H)
     share_ms, rays = [], 0
-    for k in range(n):
-        rows = rd.n_rows(H, k, n, blk)
-        ms, r = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], k * blk, H, n, row_block=blk)] * F, rows)
+    for k in range(n):  # rank k's rotated share (rtamd.dist.batch_rows), as bench.py's partition step renders it
+        sel = rd.batch_rows(H, k, n, F, blk)
+        rows = max(rd.n_rows(H, q, n, blk) for q in range(n))
+        ms, r = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], b, e, st, row_block=bl)
+                       for (b, e, st, bl) in sel], rows)
         share_ms.append(round(ms, 3))
         rays += r
     remote_rows = max(rd.n_rows(H, k, n, blk) for k in range(1, n))
@@ -697,11 +701,16 @@ def main():
     s.upload()
     B = max(1, a.frames_per_step)
     partition = a.mode == "partition"
-    # this rank's rows of every frame (partition) or whole frames (replica)
+    # this rank's rows of every frame (partition: the rotated assignment of rtamd.dist.batch_rows,
+    # frame f's blocks of residue (rank + f) mod ways, so that every rank does the same work per
+    # step) or whole frames (replica)
     ways = world if a.emulate_ranks <= 1 else a.emulate_ranks * world
     blk = max(1, a.row_block)
-    rows = rd.rank_rows(H, rank, ways, block=blk) if partition else (0, H, 1, 1)
-    n_loc = rd.n_rows(H, rank, ways, blk) if partition else H
+    frame_rows = rd.batch_rows(H, rank, ways, max(1, a.frames_per_step), blk) if partition else \
+        [(0, H, 1, 1)] * max(1, a.frames_per_step)
+    rows = frame_rows[0]
+    n_loc = sum(rd.n_rows(H, (rank + f) % ways, ways, blk) for f in range(len(frame_rows))) / len(frame_rows) \
+        if partition else H
     # gather buffers: the longest rank's row count
     n_buf = max(rd.n_rows(H, k, ways, blk) for k in range(ways)) if partition else H
     outs = [torch.empty((n_buf, W, 3), dtype=torch.float64, device="cuda") for _ in range(B)]
@@ -710,9 +719,10 @@ def main():
     out8s = [torch.zeros((B, n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
     gathered = [None, None]
     comm = torch.cuda.Stream() if world > 1 else torch.cuda.current_stream()
-    prm = s.params(W, H, kw["bdepth"], kw["intersection_only"], rows[0], rows[1], rows[2], row_block=rows[3])
+    prms = [s.params(W, H, kw["bdepth"], kw["intersection_only"], r[0], r[1], r[2], row_block=r[3]) for r in frame_rows]
+    prm = prms[0]
     stream = torch.cuda.current_stream().cuda_stream
-    gbufs = [torch.empty((B, n_buf, W, 3), dtype=torch.uint8, device="cuda") for _ in range(world)] \
+    gbufs = torch.empty((world, B, n_buf, W, 3), dtype=torch.uint8, device="cuda") \
         if rank == 0 and world > 1 and partition else None
     n_frames_rank0 = B if partition else B * world
     frames = torch.empty((n_frames_rank0, H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
@@ -726,7 +736,7 @@ def main():
         n_steps[0] += 1
         if gathered[k] is not None:  # the gathers that read these buffers two steps ago
             torch.cuda.current_stream().wait_event(gathered[k])
-        st = s.render_batch_device([prm] * B, [o.data_ptr() for o in outs], [out8s[k][f].data_ptr() for f in range(B)],
+        st = s.render_batch_device(prms, [o.data_ptr() for o in outs], [out8s[k][f].data_ptr() for f in range(B)],
                                    stream)
         rendered = torch.cuda.Event()
         rendered.record()
@@ -735,7 +745,7 @@ def main():
             if partition and ways != world:  # emulated share: no assembly
                 pass
             elif partition:  # every frame assembled on rank 0 from all ranks' rows: one gather per step
-                rd.gather_rows_batch(out8s[k], H, dst=0, out=frames, bufs=gbufs, block=blk)
+                rd.gather_rows_batch(out8s[k], H, dst=0, out=frames, bufs=gbufs, block=blk, rotate=True)
             else:
                 for f in range(B):
                     if world > 1:  # whole frames of every rank to rank 0
@@ -841,11 +851,12 @@ def main():
                        "ms_per_frame": round(elapsed / a.steps / fps * 1e3, 3),
                        "frame_latency_ms": round(latency * 1e3, 3),
                        "row_block": blk if partition else None,
-                       "parallelism": (f"EMULATED rank share: rank 0's {n_loc} of {H} rows of an {ways}-way "
+                       "parallelism": (f"EMULATED rank share: rank 0's {n_loc:g} of {H} rows per frame of an {ways}-way "
                                        f"partition, {fps} frames/step on 1 GPU (development measure, not a job)"
                                        if ways != world else
-                                       f"{fps} frames/step, each split into {blk}-row blocks interleaved over {world} GPU(s) "
-                                       f"({n_loc} rows of {H} on rank 0), pipelined renders per GPU, "
+                                       f"{fps} frames/step, each split into {blk}-row blocks interleaved over {world} GPU(s), "
+                                       f"rotated per frame (frame f: blocks of residue (rank + f) mod {world} on each rank, "
+                                       f"{n_loc:g} rows of {H} per frame on rank 0), pipelined renders per GPU, "
                                        f"{'RCCL' if a.backend == 'nccl' else 'gloo (rehearsal)'} gather "
                                        "of every frame's RGB8 rows to rank 0" if partition and world > 1 else
                                        f"1 GPU, {fps} frames/step pipelined (rt_render_batch_device)" if world == 1

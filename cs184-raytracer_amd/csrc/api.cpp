@@ -791,7 +791,7 @@ struct Render {
 			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], nullptr, ln.levels[l].lv, ln.levels[l + 1].lv,
 			                                   ln.stream));
 		HIP_TRY(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
-		                             s->stats, ln.stream));
+		                             s->stats, ln.stream, s->ctr));
 		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
 		ln.phase = Lane::FINISHING;
 		return RT_OK;

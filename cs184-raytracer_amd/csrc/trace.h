@@ -190,7 +190,7 @@ struct FusedOut {
 // lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output;
 // pixels go to their rows' outputs (fg.seg); finish non-null: the statistics finish too
 hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
-                         unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr = nullptr,
+                         unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr,
                          const FusedOut* finish = nullptr);
 // One level in one launch (k_fused): closest hits, children, and every hit's shadow rays and
 // Phong terms from registers (the level's k_closest + k_shadow + k_shade); never for

@@ -97,31 +97,42 @@ __device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, i
 	d = normalized3(dv);
 }
 
-// Chunk row q (FrameGeometry): its segment k, the last one starting at or before q (a loop
-// over the by-value descriptors with a wave-uniform bound: scalar loads of the kernel
-// arguments), the job's row ordinal and the image row, computed as the host's
-// selected_row (api.cpp).  False when the descriptor names no selected row of the frame
-// (corrupt): the caller raises DERR_ROWS and writes nothing for it.
+// Chunk row q (FrameGeometry): its segment, the last one starting at or before q, the
+// job's row ordinal, the image row (computed as the host's selected_row, api.cpp) and the
+// outputs.  The descriptors are read by a loop with a wave-uniform bound and index (scalar
+// loads of the kernel arguments, selected per lane), not by a per-lane index into the
+// argument block (which the compiler would copy to scratch).  False when the descriptor names
+// no selected row of the frame (corrupt): the caller raises DERR_ROWS and writes nothing.
 struct ChunkRowRef {
-	int32_t k, ord, row;
+	int32_t ord, row;
+	double* out;
+	uint8_t* out8;
 };
-// (The descriptors are read through an opaque pointer where they are used, so that the
-// compiler does not hoist them out of the grid-stride loops into scalar registers held
-// through the traversals.)
-__device__ __forceinline__ bool chunk_row(const FrameGeometry& fg0, int64_t q, ChunkRowRef& r) {
-	const auto* fg = uniform_ptr(opaque(&fg0));
-	int k = 0;
-	for (int j = 1; j < fg->n_segs; j++) k = q >= fg->seg[j].q0 ? j : k;
-	const auto& sg = fg->seg[k];
-	const int64_t ord = sg.ord0 + (q - sg.q0);
-	const int64_t blk = sg.row_block >= 1 ? sg.row_block : 1;
+__device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q, ChunkRowRef& r) {
+	int32_t q0 = 0, ord0 = 0, ord_end = 0, row_begin = 0, row_block = 1, row_span = 0;
+	double* out = nullptr;
+	uint8_t* out8 = nullptr;
+	// (the first index comes through an empty asm: the descriptors' loads cannot be hoisted out
+	// of the grid-stride loops into scalar registers held through the traversals)
+	int j = 0;
+	asm volatile("" : "+s"(j));
+	for (; j < fg.n_segs; j++) {
+		const RowSegment& sg = fg.seg[j];
+		if (q >= sg.q0) {
+			q0 = sg.q0, ord0 = sg.ord0, ord_end = sg.ord_end;
+			row_begin = sg.row_begin, row_block = sg.row_block, row_span = sg.row_span;
+			out = sg.out, out8 = sg.out8;
+		}
+	}
+	const int64_t ord = ord0 + (q - q0);
+	const int64_t blk = row_block >= 1 ? row_block : 1;
 	const int64_t nb = div_small(ord >= 0 ? ord : 0, blk);
-	const int64_t row = sg.row_begin + nb * sg.row_span + (ord - nb * blk);
-	r.k = k;
+	const int64_t row = row_begin + nb * row_span + (ord - nb * blk);
 	r.ord = static_cast<int32_t>(ord);
 	r.row = static_cast<int32_t>(row);
-	return q >= 0 && q < fg->n_rows && ord >= 0 && ord < sg.ord_end && sg.row_block >= 1 && row >= 0 &&
-	       row < fg->height;
+	r.out = out;
+	r.out8 = out8;
+	return q >= 0 && q < fg.n_rows && ord >= 0 && ord < ord_end && row_block >= 1 && row >= 0 && row < fg.height;
 }
 
 template <typename LV>
@@ -296,10 +307,9 @@ __device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, 
 		raise_error(ctr, DERR_ROWS);
 		return;
 	}
-	const auto& sg = uniform_ptr(opaque(&fg))->seg[rr.k];
 	const int64_t at = (static_cast<int64_t>(rr.ord) * fg.width + c) * 3;
-	double* out = sg.out;
-	uint8_t* out8 = sg.out8;
+	double* out = rr.out;
+	uint8_t* out8 = rr.out8;
 	if (out) {
 		out[at + 0] = v[0];
 		out[at + 1] = v[1];

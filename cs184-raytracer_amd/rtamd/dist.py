@@ -93,11 +93,25 @@ def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
     return None
 
 
+def batch_rows(height: int, rank: int, world: int, frames: int, block: int = 1, rotate: bool = True):
+    """This rank's row selection (rank_rows) of each of `frames` frames of one step.  rotate:
+    frame f's share is the blocks of residue (rank + f) mod world (a rotated batch): over any
+    `world` consecutive frames every rank renders every block of the image once, so with a
+    step of a multiple of `world` frames of one scene the ranks' work is equal whatever the
+    image's cost layout (the reference balances with its dynamic 2000-pixel block dispenser,
+    scene.cpp:13-24; here the assignment is static, deterministic and known to the gather)."""
+    return [rank_rows(height, rank, world, shift=(f % world) if rotate else 0, block=block) for f in range(frames)]
+
+
 def gather_rows_batch(local: torch.Tensor, height: int, dst: int = 0, out: Optional[torch.Tensor] = None,
-                      bufs: Optional[list] = None, block: int = 1) -> Optional[torch.Tensor]:
+                      bufs: Optional[torch.Tensor] = None, block: int = 1,
+                      rotate: bool = False) -> Optional[torch.Tensor]:
     """A batch of frames in ONE collective: `local` (F, n_buf, W, C) holds this rank's rows
     of F frames (n_buf >= its row count); on `dst`, out (F, H, W, C) receives every frame
-    assembled from all ranks' rows (row blocks of `block` rows, see rank_rows)."""
+    assembled from all ranks' rows (row blocks of `block` rows, see rank_rows; rotate: frame
+    f's rows of rank r are the blocks of residue (r + f) mod world, see batch_rows).  bufs: a
+    (world, F, n_buf, W, C) receive buffer on `dst` (made here when None).  The assembly is
+    one gather (index_select) over a precomputed row map, not a copy per rank and frame."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
     if world == 1:
@@ -107,15 +121,16 @@ def gather_rows_batch(local: torch.Tensor, height: int, dst: int = 0, out: Optio
     staged = local.is_cuda and dist.get_backend() == "gloo"
     src = local.cpu() if staged else local.contiguous()
     if rank == dst:
-        if bufs is None or staged:
-            bufs = [torch.empty_like(src) for _ in range(world)]
-        dist.gather(src, bufs, dst=dst)
+        shape = (world,) + tuple(src.shape)
+        if bufs is None or staged or tuple(bufs.shape) != shape:
+            bufs = torch.empty(shape, dtype=src.dtype, device=src.device)
+        dist.gather(src, list(bufs.unbind(0)), dst=dst)
+        F, n_buf = src.shape[0], src.shape[1]
         if out is None:
-            out = torch.empty((local.shape[0], height) + tuple(local.shape[2:]), dtype=local.dtype,
-                              device=local.device)
-        for r in range(world):
-            idx = _row_index(height, r, world, block, out.device)
-            out[:, idx] = bufs[r][:, : idx.numel()].to(out.device)
+            out = torch.empty((F, height) + tuple(local.shape[2:]), dtype=local.dtype, device=local.device)
+        idx = _batch_index(F, height, world, block, n_buf, rotate, bufs.device)
+        rows = torch.index_select(bufs.reshape(world * F * n_buf, -1), 0, idx)
+        out.view(F * height, -1).copy_(rows)
         return out
     dist.gather(src, None, dst=dst)
     return None
@@ -129,6 +144,24 @@ def _row_index(height, rank, world, block, device):
     if key not in _ROW_INDEX:
         _ROW_INDEX[key] = torch.tensor(rows_of(height, rank, world, block), dtype=torch.long, device=device)
     return _ROW_INDEX[key]
+
+
+_BATCH_INDEX = {}
+
+
+def _batch_index(F, height, world, block, n_buf, rotate, device):
+    """Row map of an assembled batch: entry f * height + r is the row of the gathered
+    (world, F, n_buf) buffer that holds image row r of frame f."""
+    key = (F, height, world, block, n_buf, rotate, str(device))
+    if key not in _BATCH_INDEX:
+        idx = torch.empty(F * height, dtype=torch.long)
+        for f in range(F):
+            for r in range(world):
+                k = (r + f) % world if rotate else r
+                rows = torch.tensor(rows_of(height, k, world, block), dtype=torch.long)
+                idx[f * height + rows] = (r * F + f) * n_buf + torch.arange(rows.numel())
+        _BATCH_INDEX[key] = idx.to(device)
+    return _BATCH_INDEX[key]
 
 
 def gather_frames(frame: torch.Tensor, dst: int = 0, out: Optional[list] = None) -> Optional[list]:

@@ -100,45 +100,66 @@ def test_rotated_batch_assembles_every_frame(oracle, world):
         assert np.array_equal(fr, want)
 
 
-def _batch_rows_worker(rank, world, port, scene, w, h, bdepth, block, q):
+def _batch_rows_worker(rank, world, port, scene, w, h, bdepth, block, q, rotate=False, frames=3):
     import torch.distributed as dist
     import pyoracle
     from rtamd import dist as rd
     dist.init_process_group("gloo", init_method="file://" + port, rank=rank, world_size=world)
     try:
         full, _ = pyoracle.render(scene, w, h, bdepth=bdepth, threads=2)
-        rows = rd.rows_of(h, rank, world, block)
         n_buf = max(rd.n_rows(h, k, world, block) for k in range(world))
-        local = torch.zeros((3, n_buf, w, 3), dtype=torch.float64)
-        for f in range(3):  # three frames: the image, scaled by 2 and by 3
+        local = torch.zeros((frames, n_buf, w, 3), dtype=torch.float64)
+        work = 0
+        for f, sel in enumerate(rd.batch_rows(h, rank, world, frames, block, rotate)):
+            # frame f: the image scaled by f + 1, this rank's rows of it (the selection bench.py renders)
+            rows = [r for r in range(sel[0], sel[1]) if ((r - sel[0]) // sel[3]) % sel[2] == 0]
             local[f, : len(rows)] = torch.from_numpy(full[rows] * (f + 1))
-        out = rd.gather_rows_batch(local, h, block=block)
+            work += len(rows)
+        out = rd.gather_rows_batch(local, h, block=block, rotate=rotate)
+        counts = [None] * world
+        dist.all_gather_object(counts, work)
         if rank == 0:
-            q.put(out.numpy())
+            q.put((out.numpy(), counts))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,block", [(2, 8), (3, 4), (3, 1), (8, 8), (8, 1)])
-def test_batched_row_gather(oracle, world, block):
-    """bench.py's partition step: all frames of a step gathered in one collective and
-    de-interleaved on rank 0 (row blocks)."""
+def _run_batch_rows(oracle, world, block, rotate, frames):
     w, h, bdepth = 21, 29, 3
     path = os.path.join(SCENES, "excess_inputs/bunny.rti")
     want, _ = oracle.render(path, w, h, bdepth=bdepth)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_batch_rows_worker, args=(r, world, port, path, w, h, bdepth, block, q))
+    procs = [ctx.Process(target=_batch_rows_worker, args=(r, world, port, path, w, h, bdepth, block, q, rotate, frames))
              for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got, counts = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for f in range(3):
+    for f in range(frames):
         assert np.array_equal(got[f], want * (f + 1))
+    return counts
+
+
+@pytest.mark.parametrize("world,block", [(2, 8), (3, 4), (3, 1), (8, 8), (8, 1)])
+def test_batched_row_gather(oracle, world, block):
+    """bench.py's partition step: all frames of a step gathered in one collective and
+    de-interleaved on rank 0 (row blocks)."""
+    _run_batch_rows(oracle, world, block, False, 3)
+
+
+@pytest.mark.parametrize("world,block,frames", [(2, 8, 4), (3, 4, 6), (8, 8, 16), (8, 1, 8), (8, 8, 3)])
+def test_rotated_batch_row_gather_balances_ranks(oracle, world, block, frames):
+    """bench.py's partition step with the rotated assignment (rtamd.dist.batch_rows): frame
+    f's blocks of residue (r + f) mod world go to rank r; the gather puts every row back
+    exactly, and over a multiple of `world` frames every rank renders the same rows in
+    total (the same work)."""
+    counts = _run_batch_rows(oracle, world, block, True, frames)
+    if frames % world == 0:
+        assert len(set(counts)) == 1, counts
 
 
 @pytest.mark.parametrize("scene,io,block", [("excess_inputs/refraction3.rti", False, 8), ("inputs/input-02.rti", True, 1)])

@@ -48,7 +48,7 @@ def test_native_descriptor_render(gpu, oracle, tmp_path):
     exe = tmp_path / "desc_check"
     lib = os.path.join(REPO, "cs184-raytracer_amd", "rtamd")
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe),
-                    os.path.join(REPO, "tests", "native", "desc_check.cpp"), "-L" + lib, "-lrtamd",
+                    os.path.join(REPO, "tests", "native", "desc_check.cpp"), "-L" + lib, "-lrtamd_diag",
                     "-Wl,-rpath," + lib], check=True)
     p = subprocess.run([str(exe), str(tmp_path), "render"], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout + p.stderr
