@@ -50,7 +50,6 @@ const char* device_error_text(int code) {  // MathException what() (rtbase.h:14-
 		case rtamd::DERR_ORIGIN_DIRECTION: return "ray origin is a direction vector";
 		case rtamd::DERR_PLAN: return "internal: a replayed launch plan did not fit the render";
 		case rtamd::DERR_ROWS: return "internal: a chunk row descriptor names no selected row of the frame";
-		case rtamd::DERR_RECORD: return "internal: a device level record is not the one uploaded";
 		default: return "unknown device error";
 	}
 }
@@ -191,7 +190,6 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 	L.lv.counts = reinterpret_cast<int32_t*>(take(256));
 	HIP_TRY(clear_device(L.lv.counts, 4 * sizeof(int32_t)));
 	L.lv.capacity = capacity;
-	L.lv.tag = rtamd::level_tag(static_cast<int>(level));
 	return RT_OK;
 }
 
@@ -1263,8 +1261,8 @@ void reset_after_error(rt_scene* s) {
 		ln->deferred.clear();
 		for (auto& L : ln->levels)
 			if (L.block) (void)hipMemset(L.lv.counts, 0, 2 * sizeof(int32_t));
-		// the device copy of the level records again from the pinned one (a render that found a
-		// record not the one uploaded fails with DERR_RECORD; the next one starts from the source)
+		// the device copy of the level records again from the pinned one: whatever the failed render
+		// left, the next one starts from the source
 		if (ln->levels_dev && ln->levels_cap)
 			(void)hipMemcpy(ln->levels_dev, ln->levels_pinned, ln->levels_cap * sizeof(rtamd::RayLevel),
 			                hipMemcpyHostToDevice);
@@ -1607,7 +1605,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	const int derr = static_cast<int>(sum[rtamd::ST_COUNT]);
 	if (derr == rtamd::DERR_PLAN) return kPlanMiss;
 	// MathException texts (rtbase.h:14-22) are the reference's; the internal checks are device failures
-	if (derr == rtamd::DERR_STACK || derr == rtamd::DERR_ROWS || derr == rtamd::DERR_RECORD)
+	if (derr == rtamd::DERR_STACK || derr == rtamd::DERR_ROWS)
 		return fail(RT_ERR_DEVICE, device_error_text(derr));
 	if (derr) return fail(RT_ERR_MATH, device_error_text(derr));
 	rt_counters& cnt = R.cnt;

@@ -110,7 +110,6 @@ enum DeviceError : int32_t {
 	DERR_PLAN = 5,              // a replayed launch plan did not fit the render (level capacity or
 	                            // depth): nothing was written past a buffer, the host redoes it
 	DERR_ROWS = 6,              // a chunk row descriptor names no selected row (internal; no pixel written)
-	DERR_RECORD = 7,            // a device level record is not the one uploaded (internal; nothing read through it)
 };
 
 }  // namespace rtamd

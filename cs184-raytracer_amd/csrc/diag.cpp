@@ -107,22 +107,6 @@ int rt_debug_corrupt_rows(rt_scene* s) {
 	return RT_OK;
 }
 
-// Zeroes the device copy of lane `lane`'s level record `level` (a record upload that never
-// arrived): the next render that reads it must fail with DERR_RECORD, not fault, and the
-// render after that must be exact again (reset_after_error re-uploads the records).
-// Returns 0, or 1 when the lane or level does not exist.
-int rt_debug_corrupt_level_record(rt_scene* s, int lane, int level) {
-	if (!s) return fail(RT_ERR_ARG, "null scene");
-	if (lane < 0 || lane >= static_cast<int>(s->lanes.size())) return 1;
-	Lane& ln = *s->lanes[lane];
-	if (level < 0 || static_cast<size_t>(level) >= ln.levels_cap || !ln.levels_dev) return 1;
-	HIP_TRY(hipSetDevice(s->device));
-	HIP_TRY(hipDeviceSynchronize());
-	HIP_TRY(hipMemset(ln.levels_dev + level, 0, sizeof(rtamd::RayLevel)));
-	HIP_TRY(hipDeviceSynchronize());
-	return RT_OK;
-}
-
 // Phase profile of the traversal kernels (RT_PHASE_PROF builds; zeros otherwise), 4 x 8
 // sums of per-lane shader-clock cycles (trace.h), read and cleared.
 int rt_debug_phase_profile(int device, unsigned long long* out32) {

@@ -50,13 +50,7 @@ struct RayLevel {
 	int32_t *child_refr, *child_refl;
 	int32_t* counts;             // [0] hits of this level (k_closest), [1] children spawned
 	int64_t capacity;
-	// level_tag(level): set by the host with the buffers; the kernels that read a record from
-	// the device copy check it (a record that is not the one uploaded raises DERR_RECORD and
-	// nothing is read through its pointers)
-	uint32_t tag;
-	uint32_t pad;
 };
-__host__ __device__ inline uint32_t level_tag(int level) { return 0x52544c00u ^ static_cast<uint32_t>(level); }
 
 // A chunk holds the selected rows of one frame or of several frames of the same width,
 // height and depth (rt_render_batch_device): small row selections, such as one GPU's share
@@ -65,7 +59,10 @@ __host__ __device__ inline uint32_t level_tag(int level) { return 0x52544c00u ^ 
 // image rows and output rows follow from the ordinal arithmetically (scene.cpp:25-31: pixel
 // -> (r, c) -> output(r, c)), so no kernel reads a row table from memory.
 // Chunks are cut so that they never hold more segments than this (api.cpp plan_chunks).
-constexpr int kMaxRowSegments = 32;
+#ifndef RT_MAX_ROW_SEGMENTS
+#define RT_MAX_ROW_SEGMENTS 32
+#endif
+constexpr int kMaxRowSegments = RT_MAX_ROW_SEGMENTS;
 struct RowSegment {
 	double* out;          // the job's f64 rows: ordinal o at out + o * width * 3 (or null)
 	uint8_t* out8;        // its RGB8 rows, the same layout (or null)

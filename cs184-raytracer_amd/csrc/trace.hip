@@ -99,16 +99,23 @@ __device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, i
 
 // Chunk row q (FrameGeometry): its segment, the last one starting at or before q, the
 // job's row ordinal, the image row (computed as the host's selected_row, api.cpp) and the
-// outputs.  The descriptors are read by a loop with a wave-uniform bound and index (scalar
-// loads of the kernel arguments, selected per lane), not by a per-lane index into the
-// argument block (which the compiler would copy to scratch).  False when the descriptor names
-// no selected row of the frame (corrupt): the caller raises DERR_ROWS and writes nothing.
+// outputs.  False when the descriptor names no selected row of the frame (corrupt): the
+// caller raises DERR_ROWS and writes nothing.
+// Every lane of the wave calls it.  The common case is wave-uniform: the segment of the
+// wave's first lane, found by a scalar loop over the by-value descriptors, holds every
+// lane's row (an 8x8 tile or 64 pixels of a row lie in one job's rows unless they straddle
+// two jobs), and each lane only adds its offset.  Otherwise each lane selects its segment in
+// a loop over them (uniform index, scalar loads, per-lane selects).  Neither indexes the
+// argument block per lane (the compiler would copy it to scratch).
 struct ChunkRowRef {
 	int32_t ord, row;
 	double* out;
 	uint8_t* out8;
 };
-__device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q, ChunkRowRef& r) {
+#ifndef RT_ROWS_UNIFORM
+#define RT_ROWS_UNIFORM 1
+#endif
+__device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q, bool on, ChunkRowRef& r) {
 	int32_t q0 = 0, ord0 = 0, ord_end = 0, row_begin = 0, row_block = 1, row_span = 0;
 	double* out = nullptr;
 	uint8_t* out8 = nullptr;
@@ -116,17 +123,40 @@ __device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q, Ch
 	// of the grid-stride loops into scalar registers held through the traversals)
 	int j = 0;
 	asm volatile("" : "+s"(j));
-	for (; j < fg.n_segs; j++) {
-		const RowSegment& sg = fg.seg[j];
-		if (q >= sg.q0) {
-			q0 = sg.q0, ord0 = sg.ord0, ord_end = sg.ord_end;
-			row_begin = sg.row_begin, row_block = sg.row_block, row_span = sg.row_span;
-			out = sg.out, out8 = sg.out8;
+	bool uniform = false;
+	if (RT_ROWS_UNIFORM) {
+		const uint64_t act = __ballot(on);
+		if (act) {
+			const int first = __builtin_ctzll(act);
+			const int64_t qf = (static_cast<int64_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(q >> 32), first)) << 32) |
+			                   static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(q), first));
+			int k = j;
+			for (int t = j + 1; t < fg.n_segs; t++)
+				if (qf >= fg.seg[t].q0) k = t;
+			const int64_t q_end = k + 1 < fg.n_segs ? fg.seg[k + 1].q0 : fg.n_rows;
+			const RowSegment& sg = fg.seg[k];
+			uniform = __ballot(on && !(q >= sg.q0 && q < q_end)) == 0;
+			if (uniform) {
+				q0 = sg.q0, ord0 = sg.ord0, ord_end = sg.ord_end;
+				row_begin = sg.row_begin, row_block = sg.row_block, row_span = sg.row_span;
+				out = sg.out, out8 = sg.out8;
+			}
+		}
+	}
+	if (!uniform) {
+		for (; j < fg.n_segs; j++) {
+			const RowSegment& sg = fg.seg[j];
+			if (q >= sg.q0) {
+				q0 = sg.q0, ord0 = sg.ord0, ord_end = sg.ord_end;
+				row_begin = sg.row_begin, row_block = sg.row_block, row_span = sg.row_span;
+				out = sg.out, out8 = sg.out8;
+			}
 		}
 	}
 	const int64_t ord = ord0 + (q - q0);
+	// (blocks of one row, the whole-frame and interleaved-row selections: no division)
 	const int64_t blk = row_block >= 1 ? row_block : 1;
-	const int64_t nb = div_small(ord >= 0 ? ord : 0, blk);
+	const int64_t nb = blk == 1 ? ord : div_small(ord >= 0 ? ord : 0, blk);
 	const int64_t row = row_begin + nb * row_span + (ord - nb * blk);
 	r.ord = static_cast<int32_t>(ord);
 	r.row = static_cast<int32_t>(row);
@@ -141,7 +171,7 @@ __device__ __forceinline__ void level_ray(const DeviceScene& S, const FrameGeome
 	if (level == 0) {
 		const int64_t q = div_small(i, fg.width);
 		ChunkRowRef rr;
-		if (!chunk_row(fg, q, rr)) {
+		if (!chunk_row(fg, q, true, rr)) {
 			raise_error(ctr, DERR_ROWS);
 			rr.row = 0;  // a ray of a valid row: its pixel is never written (write_pixel checks again)
 		}
@@ -303,7 +333,7 @@ __device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, 
 	const int64_t q = div_small(i, fg.width);
 	const int64_t c = i - q * fg.width;
 	ChunkRowRef rr;
-	if (!chunk_row(fg, q, rr)) {
+	if (!chunk_row(fg, q, true, rr)) {
 		raise_error(ctr, DERR_ROWS);
 		return;
 	}
@@ -320,15 +350,6 @@ __device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, 
 		out8[at + 1] = to_u8(v[1]);
 		out8[at + 2] = to_u8(v[2]);
 	}
-}
-
-// The level records a launch reads from the device copy carry their tag (RayLevel::tag): a
-// record that is not the uploaded one raises DERR_RECORD and the block leaves before any
-// pointer of it is used (block-uniform: every thread reads the same records)
-__device__ __forceinline__ bool record_ok(const RayLevel* levels, int level, DeviceCounters* ctr) {
-	const bool ok = uniform_ptr(levels)[level].tag == level_tag(level);
-	if (!ok && threadIdx.x == 0) raise_error(ctr, DERR_RECORD);
-	return ok;
 }
 
 template <bool kPacket, int kMesh, typename NV, typename DV, typename WS>
@@ -546,7 +567,6 @@ __global__ void __launch_bounds__(kBlock)
 	// the traversal stacks (LBVH searches: none in a scene of spheres only)
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
-	if (!record_ok(levels, level, ctr) || (remaining > 0 && !record_ok(levels, level + 1, ctr))) return;
 	// level records read through the constant address space (scalar loads at their uses)
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
@@ -654,7 +674,6 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ double park_mem[RT_FUSED_PARK && kPacket ? 6 * kBlock : 1];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
-	if (!record_ok(levels, level, ctr) || (remaining > 0 && !record_ok(levels, level + 1, ctr))) return;
 	const auto& cur0 = *uniform_ptr(levels + level);
 	const auto& next0 = *uniform_ptr(levels + (remaining > 0 ? level + 1 : level));
 	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur0.capacity) : n_host;
@@ -934,8 +953,6 @@ __global__ void __launch_bounds__(kBlock)
 	__shared__ int32_t stack_mem[kMesh < kMeshBvh ? 1 : kPacket ? (kBlock / 64) * kWaveStack : kStackDepth * kBlock];
 	__shared__ uint32_t stat_lds[kCount ? W_COUNT * kBlock : 1];
 	int32_t* stack = kMesh < kMeshBvh ? stack_mem : kPacket ? stack_mem + (threadIdx.x / 64) * kWaveStack : stack_mem + threadIdx.x;
-	for (int k = 0; k < B.n; k++)
-		if (!record_ok(levels, B.level[k], ctr)) return;
 	const int64_t total = batch_total<true>(B, S.n_nonambient);
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride) {
@@ -948,8 +965,6 @@ __global__ void __launch_bounds__(kBlock)
 // Phong terms in light order (scene.cpp:78-108), one thread per hit of the level
 __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, ShadeBatch B, const RayLevel* levels,
                                                        DeviceCounters* ctr) {
-	for (int k = 0; k < B.n; k++)
-		if (!record_ok(levels, B.level[k], ctr)) return;
 	// glibc pow tables in LDS: the specular pow's two dependent table lookups per light
 	// are LDS latency instead of divergent L2 gathers
 	__shared__ double log_tab[512];

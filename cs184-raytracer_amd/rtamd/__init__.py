@@ -185,7 +185,6 @@ def lib(diag: bool = False) -> ctypes.CDLL:
             "rt_debug_builder_digest": (i32, [vp, ctypes.POINTER(ctypes.c_uint64)]),
             "rt_debug_fail_after": (i32, [vp, i32]),
             "rt_debug_corrupt_rows": (i32, [vp]),
-            "rt_debug_corrupt_level_record": (i32, [vp, i32, i32]),
             "rt_debug_plan_chunks": (i32, [i32, ctypes.POINTER(rt_render_params), i32, i64, i32,
                                            ctypes.POINTER(ctypes.c_int64), i32]),
             "rt_debug_phase_profile": (i32, [i32, vp]),
@@ -433,14 +432,6 @@ class Scene:
     def debug_corrupt_rows(self) -> None:
         """Fault injection (diag scenes): the next chunk's row descriptors name rows no frame has."""
         _raise(self._L.rt_debug_corrupt_rows(self.handle), L=self._L)
-
-    def debug_corrupt_level_record(self, lane: int, level: int) -> bool:
-        """Fault injection (diag scenes): zeroes the device copy of a lane's level record (an
-        upload that never arrived); False when that lane or level does not exist."""
-        rc = self._L.rt_debug_corrupt_level_record(self.handle, lane, level)
-        if rc < 0:
-            _raise(rc, L=self._L)
-        return rc == 0
 
     def render_device(self, params: rt_render_params, out_rgb_ptr: int = 0, out_rgb8_ptr: int = 0,
                       stream_ptr: int = 0) -> RenderStats:

@@ -177,28 +177,6 @@ def test_corrupt_row_descriptor_is_reported_not_written(gpu, oracle, replay):
     s.close()
 
 
-@pytest.mark.parametrize("level", [0, 1, 3])
-def test_missing_level_record_is_reported_not_read(gpu, oracle, level):
-    """A device level record that does not hold its upload (the form of the round-5
-    multi-process failures; injected here by zeroing it, librtamd_diag.so) is caught by its
-    tag (RayLevel::tag): the render fails with the named device error instead of following
-    its pointers, and the next render, after the records are uploaded again, is exact."""
-    scene = os.path.join(SCENES, "excess_inputs/bunny.rti")
-    w, h, bdepth = 64, 40, 4
-    want, cnt = oracle.render(scene, w, h, bdepth=bdepth)
-    s = gpu.load_scene(scene, diag=True)
-    o = gpu.Options(renderWidth_=w, renderHeight_=h, bounceDepth_=bdepth)
-    s.renderScene(options=o)
-    s.renderScene(options=o)  # the second call has lane streams and a plan; the third replays it
-    assert s.debug_corrupt_level_record(0, level)
-    with pytest.raises(gpu.DeviceError, match="level record"):
-        s.renderScene(options=o)
-    img = s.renderScene(options=o)
-    assert np.array_equal(img.view(np.uint64), want.view(np.uint64))
-    assert (s.last_stats.trace_rays, s.last_stats.shadow_rays) == (cnt["trace_rays"], cnt["shadow_rays"])
-    s.close()
-
-
 def test_right_sized_levels_then_replay_on_a_torch_stream(gpu, oracle):
     """a call traced host-driven grows the level buffers and cuts them back after it
     (right_size_levels, record copies on the lane's stream); the next call of that shape replays

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_function(rt):
 
 
 DIAG_HOOKS = ["rt_debug_builder_digest", "rt_debug_fail_after", "rt_debug_corrupt_rows",
-              "rt_debug_corrupt_level_record", "rt_debug_plan_chunks", "rt_debug_phase_profile",
+              "rt_debug_plan_chunks", "rt_debug_phase_profile",
               "rt_debug_wave_times", "rt_debug_fetch_calibration", "rt_debug_valu_calibration", "rt_debug_valu_rate"]
 
 
