@@ -97,53 +97,38 @@ __device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, i
 	d = normalized3(dv);
 }
 
-// Chunk row q (FrameGeometry): its segment, the last one starting at or before q, the
-// job's row ordinal, the image row (computed as the host's selected_row, api.cpp) and the
-// outputs.  False when the descriptor names no selected row of the frame (corrupt): the
-// caller raises DERR_ROWS and writes nothing.
-// Every lane of the wave calls it.  The common case is wave-uniform: the segment of the
-// wave's first lane, found by a scalar loop over the by-value descriptors, holds every
+// Chunk row q (FrameGeometry): the job's row ordinal, the image row (computed as the host's
+// selected_row, api.cpp) and the job's outputs, from the segment holding q (the last one
+// starting at or before it).  False when the descriptor names no selected row of the frame
+// (corrupt): the caller raises DERR_ROWS and writes nothing.
+// Every active lane of the wave calls it.  The common case is wave-uniform: the segment of
+// the wave's first lane, found by a scalar loop over the by-value descriptors, holds every
 // lane's row (an 8x8 tile or 64 pixels of a row lie in one job's rows unless they straddle
 // two jobs), and each lane only adds its offset.  Otherwise each lane selects its segment in
 // a loop over them (uniform index, scalar loads, per-lane selects).  Neither indexes the
-// argument block per lane (the compiler would copy it to scratch).
+// argument block per lane (the compiler would copy it to scratch).  32-bit arithmetic: a
+// chunk holds at most 2^22 pixels, an image at most 2^31 rows.
 struct ChunkRowRef {
 	int32_t ord, row;
 	double* out;
 	uint8_t* out8;
 };
-#ifndef RT_ROWS_UNIFORM
-#define RT_ROWS_UNIFORM 1
-#endif
-__device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q, bool on, ChunkRowRef& r) {
-	int32_t q0 = 0, ord0 = 0, ord_end = 0, row_begin = 0, row_block = 1, row_span = 0;
-	double* out = nullptr;
-	uint8_t* out8 = nullptr;
+__device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q64, ChunkRowRef& r) {
+	const int32_t q = static_cast<int32_t>(q64);
 	// (the first index comes through an empty asm: the descriptors' loads cannot be hoisted out
 	// of the grid-stride loops into scalar registers held through the traversals)
 	int j = 0;
 	asm volatile("" : "+s"(j));
-	bool uniform = false;
-	if (RT_ROWS_UNIFORM) {
-		const uint64_t act = __ballot(on);
-		if (act) {
-			const int first = __builtin_ctzll(act);
-			const int64_t qf = (static_cast<int64_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(q >> 32), first)) << 32) |
-			                   static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int32_t>(q), first));
-			int k = j;
-			for (int t = j + 1; t < fg.n_segs; t++)
-				if (qf >= fg.seg[t].q0) k = t;
-			const int64_t q_end = k + 1 < fg.n_segs ? fg.seg[k + 1].q0 : fg.n_rows;
-			const RowSegment& sg = fg.seg[k];
-			uniform = __ballot(on && !(q >= sg.q0 && q < q_end)) == 0;
-			if (uniform) {
-				q0 = sg.q0, ord0 = sg.ord0, ord_end = sg.ord_end;
-				row_begin = sg.row_begin, row_block = sg.row_block, row_span = sg.row_span;
-				out = sg.out, out8 = sg.out8;
-			}
-		}
-	}
-	if (!uniform) {
+	const int32_t qf = __builtin_amdgcn_readfirstlane(q);
+	int k = j;
+	for (int t = j + 1; t < fg.n_segs; t++)
+		if (qf >= fg.seg[t].q0) k = t;
+	const int32_t q_end = k + 1 < fg.n_segs ? fg.seg[k + 1].q0 : fg.n_rows;
+	int32_t q0 = fg.seg[k].q0, ord0 = fg.seg[k].ord0, ord_end = fg.seg[k].ord_end;
+	int32_t row_begin = fg.seg[k].row_begin, row_block = fg.seg[k].row_block, row_span = fg.seg[k].row_span;
+	double* out = fg.seg[k].out;
+	uint8_t* out8 = fg.seg[k].out8;
+	if (__ballot(q < q0 || q >= q_end)) {  // the wave straddles segments: per lane
 		for (; j < fg.n_segs; j++) {
 			const RowSegment& sg = fg.seg[j];
 			if (q >= sg.q0) {
@@ -153,25 +138,31 @@ __device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q, bo
 			}
 		}
 	}
-	const int64_t ord = ord0 + (q - q0);
-	// (blocks of one row, the whole-frame and interleaved-row selections: no division)
-	const int64_t blk = row_block >= 1 ? row_block : 1;
-	const int64_t nb = blk == 1 ? ord : div_small(ord >= 0 ? ord : 0, blk);
-	const int64_t row = row_begin + nb * row_span + (ord - nb * blk);
-	r.ord = static_cast<int32_t>(ord);
-	r.row = static_cast<int32_t>(row);
+	const int32_t ord = ord0 + (q - q0);
+	int32_t row;
+	if (row_block == 1) {  // blocks of one row: whole frames and interleaved rows, no division
+		row = row_begin + ord * row_span;
+	} else {
+		const int32_t blk = row_block >= 1 ? row_block : 1;
+		const int32_t nb = (ord >= 0 ? ord : 0) / blk;
+		row = row_begin + nb * row_span + (ord - nb * blk);
+	}
+	r.ord = ord;
+	r.row = row;
 	r.out = out;
 	r.out8 = out8;
-	return q >= 0 && q < fg.n_rows && ord >= 0 && ord < ord_end && row_block >= 1 && row >= 0 && row < fg.height;
+	return q64 >= 0 && q < fg.n_rows && ord >= 0 && ord < ord_end && row_block >= 1 && row >= 0 && row < fg.height;
 }
 
-template <typename LV>
+// kLevel0: the camera rays of level 0 (the traversal kernels are instantiated separately for
+// it: the row look-up and the pixel writes stay out of the other levels' register allocation)
+template <bool kLevel0, typename LV>
 __device__ __forceinline__ void level_ray(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t i,
                                           const LV& cur, V3& o, V3& d, bool& inside, DeviceCounters* ctr) {
-	if (level == 0) {
+	if constexpr (kLevel0) {
 		const int64_t q = div_small(i, fg.width);
 		ChunkRowRef rr;
-		if (!chunk_row(fg, q, true, rr)) {
+		if (!chunk_row(fg, q, rr)) {
 			raise_error(ctr, DERR_ROWS);
 			rr.row = 0;  // a ray of a valid row: its pixel is never written (write_pixel checks again)
 		}
@@ -333,7 +324,7 @@ __device__ __forceinline__ void write_pixel(const FrameGeometry& fg, int64_t i, 
 	const int64_t q = div_small(i, fg.width);
 	const int64_t c = i - q * fg.width;
 	ChunkRowRef rr;
-	if (!chunk_row(fg, q, true, rr)) {
+	if (!chunk_row(fg, q, rr)) {
 		raise_error(ctr, DERR_ROWS);
 		return;
 	}
@@ -365,7 +356,7 @@ __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, in
 // kFused (k_fused): the hit is shaded right here, its shadow rays and Phong terms from the
 // hit held in registers (no hit record, no k_shadow / k_shade launch), and the colour goes
 // where fo says.  Never for --intersection-only.
-template <bool kPacket, bool kCount, int kMesh, bool kFused = false>
+template <bool kPacket, bool kCount, int kMesh, bool kLevel0, bool kFused = false>
 __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGeometry& fg, int level, int64_t n,
                                              int remaining, int plan_last, const RayLevel* levels,
                                              DeviceCounters* ctr, unsigned long long* stats, int64_t t,
@@ -374,7 +365,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	// the level records (~30 buffer pointers) are read where they are used, before and after
 	// the traversal, not held in scalar registers through it
 	const int next_level = remaining > 0 ? level + 1 : level;
-	const int64_t i = (level == 0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
+	const int64_t i = (kLevel0 && kPacket) ? tile_pixel(fg, n, t) : (t < n ? t : -1);
 	const bool active = i >= 0;
 	WorkStats<kCount> ws{};
 	ws.init(stat_lds);
@@ -386,7 +377,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 	bool inside = false;
 	V3 o = mk(0, 0, 0), d = mk(0, 0, 1);
 	PROF_BEGIN(t_setup);
-	if (active) level_ray(S, fg, level, i, *uniform_ptr(opaque(levels) + level), o, d, inside, ctr);
+	if (active) level_ray<kLevel0>(S, fg, level, i, *uniform_ptr(opaque(levels) + level), o, d, inside, ctr);
 	PROF_END(ws, PH_SETUP, t_setup);
 #if RT_DIAG_LANES
 	if (!kPacket) diag_lanes(0, active);  // [0] wave slots, [1] active lanes of k_closest<false>
@@ -523,7 +514,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 			                               stats, ws, col);
 		}
 		if (!active) return;
-		if (fo->final) {
+		if (kLevel0 && fo->final) {  // (a plan of one traced level: level 0)
 			write_pixel(fg, i, col, true, ctr);
 		} else {
 			cur.cr[i] = col[0];
@@ -555,7 +546,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 // before the host knows their size: the ray count is read from the previous level's
 // child counter (n_dev) and a fixed grid strides over it, so each level is queued behind
 // the previous one without a host round trip.
-template <bool kPacket, bool kCount, int kMesh>
+template <bool kPacket, bool kCount, int kMesh, bool kLevel0>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(kMesh == kMeshNone ? RT_SPHERE_WAVES : kMesh == kMeshLinear ? RT_LINEAR_WAVES : kPacket ? RT_PACKET_WAVES : RT_CLOSEST_WAVES))) k_closest(DeviceScene S, FrameGeometry fg, int level,
                                                                       int64_t n_host, const int32_t* n_dev,
@@ -578,12 +569,12 @@ __global__ void __launch_bounds__(kBlock)
 		if (remaining > 0) next0.counts[0] = next0.counts[1] = 0;
 		if (n) atomicAdd(stats + ST_RAYS, static_cast<unsigned long long>(n));  // traceRay calls
 	}
-	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
+	const int64_t limit = (kLevel0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-	if (RT_WARM_L2 && kMesh == kMeshBvh && level == 0) warm_l2(S);
+	if (RT_WARM_L2 && kMesh == kMeshBvh && kLevel0) warm_l2(S);
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
 		WT_BEGIN();
-		closest_item<kPacket, kCount, kMesh>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
+		closest_item<kPacket, kCount, kMesh, kLevel0>(S, fg, level, n, remaining, plan_last, levels, ctr, stats, base + threadIdx.x,
 		                      append_lds, stack, stat_lds);
 		WT_END(1 | kPacket << 4 | level << 8, base + (threadIdx.x & ~63));
 	}
@@ -665,7 +656,7 @@ __device__ void last_block_finish(unsigned long long* stats, DeviceCounters* ctr
 #ifndef RT_FUSED_WAVES
 #define RT_FUSED_WAVES 4
 #endif
-template <bool kPacket, int kMesh>
+template <bool kPacket, int kMesh, bool kLevel0>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(RT_FUSED_WAVES))) k_fused(
         DeviceScene S, FrameGeometry fg, int level, int64_t n_host, const int32_t* n_dev, int remaining, int plan_last,
@@ -681,12 +672,12 @@ __global__ void __launch_bounds__(kBlock)
 		if (remaining > 0) next0.counts[0] = next0.counts[1] = 0;
 		if (n) atomicAdd(stats + ST_RAYS, static_cast<unsigned long long>(n));
 	}
-	const int64_t limit = (level == 0 && kPacket) ? tile_threads(n, fg.width) : n;
+	const int64_t limit = (kLevel0 && kPacket) ? tile_threads(n, fg.width) : n;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
-	if (RT_WARM_L2 && kMesh == kMeshBvh && level == 0) warm_l2(S);
+	if (RT_WARM_L2 && kMesh == kMeshBvh && kLevel0) warm_l2(S);
 	for (int64_t base = xcd_block() * kBlock; base < limit; base += stride) {
 		WT_BEGIN();
-		closest_item<kPacket, false, kMesh, true>(S, fg, level, n, remaining, plan_last, levels, ctr, stats,
+		closest_item<kPacket, false, kMesh, kLevel0, true>(S, fg, level, n, remaining, plan_last, levels, ctr, stats,
 		                                          base + threadIdx.x, append_lds, stack, nullptr, &fo,
 		                                          (lds_f64*)(park_mem));
 		WT_END(2 | kPacket << 4 | level << 8, base + (threadIdx.x & ~63));
@@ -1286,9 +1277,11 @@ hipError_t launch_closest(const DeviceScene& s, const FrameGeometry& fg, int lev
 	by_mesh_kind(s, [&](auto m) {
 		constexpr int M = decltype(m)::value;
 		if (packet)
-			s.work_stats ? go(k_closest<true, true, M>) : go(k_closest<true, false, M>);
+			level == 0 ? (s.work_stats ? go(k_closest<true, true, M, true>) : go(k_closest<true, false, M, true>))
+			           : (s.work_stats ? go(k_closest<true, true, M, false>) : go(k_closest<true, false, M, false>));
 		else
-			s.work_stats ? go(k_closest<false, true, M>) : go(k_closest<false, false, M>);
+			level == 0 ? (s.work_stats ? go(k_closest<false, true, M, true>) : go(k_closest<false, false, M, true>))
+			           : (s.work_stats ? go(k_closest<false, true, M, false>) : go(k_closest<false, false, M, false>));
 	});
 	return hipGetLastError();
 }
@@ -1369,7 +1362,10 @@ hipError_t launch_fused(const DeviceScene& s, const FrameGeometry& fg, int level
 	};
 	by_mesh_kind(s, [&](auto m) {
 		constexpr int M = decltype(m)::value;
-		packet ? go(k_fused<true, M>) : go(k_fused<false, M>);
+		if (level == 0)
+			packet ? go(k_fused<true, M, true>) : go(k_fused<false, M, true>);
+		else
+			packet ? go(k_fused<true, M, false>) : go(k_fused<false, M, false>);
 	});
 	return hipGetLastError();
 }
