@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--row-block", type=int, default=8,
                     help="partition granularity: blocks of this many rows interleaved over the ranks (8 = the "
                          "8x8 ray tiles stay whole)")
+    ap.add_argument("--batch-block", type=int, default=0,
+                    help="partition of a multi-frame step: blocks of this many rows, rotated per frame (0 = one "
+                         "contiguous band of whole 8-row tiles per rank, rtamd.dist.band_rows)")
     ap.add_argument("--frames-per-step", type=int, default=48,
                     help="frames per step (partition: in total, every frame split over the ranks; "
                          "replica: per rank)")
@@ -535,18 +538,22 @@ def emulated_batch_partition(a, s, W, H, kw, blk, cfg, torch, n=8):
 
     whole_ms, whole_rays = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], 0, H, 1)] * F, H)
     share_ms, rays = [], 0
+    bblk = a.batch_block if a.batch_block > 0 else rd.band_rows(H, n)
     for k in range(n):  # rank k's rotated share (rtamd.dist.batch_rows), as bench.py's partition step renders it
-        sel = rd.batch_rows(H, k, n, F, blk)
-        rows = max(rd.n_rows(H, q, n, blk) for q in range(n))
+        sel = rd.batch_rows(H, k, n, F, bblk)
+        rows = max(rd.n_rows(H, q, n, bblk) for q in range(n))
         ms, r = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], b, e, st, row_block=bl)
                        for (b, e, st, bl) in sel], rows)
         share_ms.append(round(ms, 3))
         rays += r
-    remote_rows = max(rd.n_rows(H, k, n, blk) for k in range(1, n))
+    remote_rows = max(rd.n_rows(H, k, n, bblk) for k in range(1, n))
     gather_ms = F * remote_rows * W * 3 / (XGMI_LINK_GBS * 1e9) * 1e3 + XGMI_FIXED_US / 1e3
     node_ms = max(max(share_ms), gather_ms)
     serial_ms = max(share_ms) + gather_ms
-    return {"frames_per_step": F, "n_gpus": n, "one_gpu_batch_ms": round(whole_ms, 3),
+    return {"frames_per_step": F, "n_gpus": n, "rows_per_block": bblk,
+            "partition": f"{bblk}-row blocks ({'one contiguous band per rank' if bblk == rd.band_rows(H, n) else 'interleaved'}), "
+                         f"rotated per frame: frame f's blocks of residue (rank + f) mod {n} on rank k",
+            "one_gpu_batch_ms": round(whole_ms, 3),
             "one_gpu_mrays_per_s": round(whole_rays / whole_ms / 1e3, 1),
             "share_ms_per_rank": share_ms, "max_share_ms": max(share_ms),
             "imbalance": round(max(share_ms) / (sum(share_ms) / n), 3), "gather_ms_assumed": round(gather_ms, 3),
@@ -705,7 +712,7 @@ def main():
     # frame f's blocks of residue (rank + f) mod ways, so that every rank does the same work per
     # step) or whole frames (replica)
     ways = world if a.emulate_ranks <= 1 else a.emulate_ranks * world
-    blk = max(1, a.row_block)
+    blk = a.batch_block if a.batch_block > 0 else rd.band_rows(H, ways)
     frame_rows = rd.batch_rows(H, rank, ways, max(1, a.frames_per_step), blk) if partition else \
         [(0, H, 1, 1)] * max(1, a.frames_per_step)
     rows = frame_rows[0]
@@ -854,7 +861,8 @@ def main():
                        "parallelism": (f"EMULATED rank share: rank 0's {n_loc:g} of {H} rows per frame of an {ways}-way "
                                        f"partition, {fps} frames/step on 1 GPU (development measure, not a job)"
                                        if ways != world else
-                                       f"{fps} frames/step, each split into {blk}-row blocks interleaved over {world} GPU(s), "
+                                       f"{fps} frames/step, each split into {blk}-row blocks over {world} GPU(s) "
+                                       f"({'one contiguous band per GPU' if blk == rd.band_rows(H, world) else 'interleaved'}), "
                                        f"rotated per frame (frame f: blocks of residue (rank + f) mod {world} on each rank, "
                                        f"{n_loc:g} rows of {H} per frame on rank 0), pipelined renders per GPU, "
                                        f"{'RCCL' if a.backend == 'nccl' else 'gloo (rehearsal)'} gather "

@@ -102,7 +102,7 @@ __device__ __forceinline__ void primary_ray(const DCamera* camp, int r, int c, i
 // starting at or before it).  False when the descriptor names no selected row of the frame
 // (corrupt): the caller raises DERR_ROWS and writes nothing.
 // Every active lane of the wave calls it.  The common case is wave-uniform: the segment of
-// the wave's first lane, found by a scalar loop over the by-value descriptors, holds every
+// the wave's first lane, found by a scalar search of the by-value descriptors, holds every
 // lane's row (an 8x8 tile or 64 pixels of a row lie in one job's rows unless they straddle
 // two jobs), and each lane only adds its offset.  Otherwise each lane selects its segment in
 // a loop over them (uniform index, scalar loads, per-lane selects).  Neither indexes the
@@ -120,9 +120,16 @@ __device__ __forceinline__ bool chunk_row(const FrameGeometry& fg, int64_t q64, 
 	int j = 0;
 	asm volatile("" : "+s"(j));
 	const int32_t qf = __builtin_amdgcn_readfirstlane(q);
-	int k = j;
-	for (int t = j + 1; t < fg.n_segs; t++)
-		if (qf >= fg.seg[t].q0) k = t;
+	// binary search (scalar): the last segment starting at or before qf, in log2(n_segs)
+	// dependent loads rather than n_segs (a GPU's row share of 16 frames is 16 segments)
+	int k = j, hi = fg.n_segs - 1;
+	while (k < hi) {
+		const int mid = (k + hi + 1) >> 1;
+		if (fg.seg[mid].q0 <= qf)
+			k = mid;
+		else
+			hi = mid - 1;
+	}
 	const int32_t q_end = k + 1 < fg.n_segs ? fg.seg[k + 1].q0 : fg.n_rows;
 	int32_t q0 = fg.seg[k].q0, ord0 = fg.seg[k].ord0, ord_end = fg.seg[k].ord_end;
 	int32_t row_begin = fg.seg[k].row_begin, row_block = fg.seg[k].row_block, row_span = fg.seg[k].row_span;

@@ -93,13 +93,22 @@ def gather_rows(local: torch.Tensor, height: int, dst: int = 0,
     return None
 
 
+def band_rows(height: int, world: int, tile: int = 8) -> int:
+    """Rows of one band when a frame is cut into `world` contiguous bands of whole 8-row ray
+    tiles (the last band takes the rest): the block size of the multi-frame partition."""
+    return max(tile, -(-height // (world * tile)) * tile)
+
+
 def batch_rows(height: int, rank: int, world: int, frames: int, block: int = 1, rotate: bool = True):
     """This rank's row selection (rank_rows) of each of `frames` frames of one step.  rotate:
     frame f's share is the blocks of residue (rank + f) mod world (a rotated batch): over any
     `world` consecutive frames every rank renders every block of the image once, so with a
     step of a multiple of `world` frames of one scene the ranks' work is equal whatever the
     image's cost layout (the reference balances with its dynamic 2000-pixel block dispenser,
-    scene.cpp:13-24; here the assignment is static, deterministic and known to the gather)."""
+    scene.cpp:13-24; here the assignment is static, deterministic and known to the gather).
+    With block = band_rows(height, world) each share is one contiguous band of the frame: the
+    rows a GPU traces at once lie together in the image (L2 locality of the scene), and the
+    rotation balances the bands' unequal costs over the step."""
     return [rank_rows(height, rank, world, shift=(f % world) if rotate else 0, block=block) for f in range(frames)]
 
 

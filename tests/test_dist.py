@@ -151,12 +151,16 @@ def test_batched_row_gather(oracle, world, block):
     _run_batch_rows(oracle, world, block, False, 3)
 
 
-@pytest.mark.parametrize("world,block,frames", [(2, 8, 4), (3, 4, 6), (8, 8, 16), (8, 1, 8), (8, 8, 3)])
+@pytest.mark.parametrize("world,block,frames", [(2, 8, 4), (3, 4, 6), (8, 8, 16), (8, 1, 8), (8, 8, 3),
+                                               (2, "band", 4), (3, "band", 3), (8, "band", 8)])
 def test_rotated_batch_row_gather_balances_ranks(oracle, world, block, frames):
     """bench.py's partition step with the rotated assignment (rtamd.dist.batch_rows): frame
     f's blocks of residue (r + f) mod world go to rank r; the gather puts every row back
     exactly, and over a multiple of `world` frames every rank renders the same rows in
     total (the same work)."""
+    if block == "band":  # bench.py's default: one contiguous band of whole 8-row tiles per rank
+        from rtamd import dist as rd
+        block = rd.band_rows(29, world)
     counts = _run_batch_rows(oracle, world, block, True, frames)
     if frames % world == 0:
         assert len(set(counts)) == 1, counts
