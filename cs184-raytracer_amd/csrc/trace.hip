@@ -865,7 +865,14 @@ __device__ __forceinline__ void shade_in_place(const DeviceScene& S, bool on, in
 //    towards each light in turn (one light at a time, still wave-uniform), loading the hit
 //    records once for all lights.
 // The light record of the wave is read with scalar loads.
-template <bool kPacket, bool kCount, int kMesh>
+// Fused shading (ShadeBatch::fused, all lights per lane): the lane computes its hit's Phong
+// terms from the verdicts held in registers (no k_shade).  kFuse: 1 the kernel always fuses (its
+// own instantiation, without the light-major index mapping and the verdict stores: +0.6% on
+// the batch bench), 0 never (per-lane kernels with LBVH searches), 2 as B.fused says.  The
+// packet kernel's unfused launches (light-major, single frames) keep the form with both paths:
+// an instantiation without the Phong terms finished its launches sooner and moved their k_shade
+// onto the CUs the closest-hit chain needs (C3 frame 1.207 vs 1.169 ms, A/B).
+template <bool kPacket, bool kCount, int kMesh, int kFuse>
 __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBatch& B, const RayLevel* levels,
                                             DeviceCounters* ctr, unsigned long long* stats, int64_t tg, int32_t* stack,
                                             uint32_t* stat_lds) {
@@ -878,7 +885,8 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	PROF_BEGIN(t_total);
 	int j0 = 0, j1 = nl;
 	int64_t h = t;
-	if (!B.all_lights) {
+	const bool fused = kFuse == 1 || (kFuse == 2 && B.fused);
+	if (kFuse != 1 && !B.all_lights) {
 		const int64_t nh64 = (nh + 63) & ~int64_t(63);
 		// the wave's light: j = t0 / nh64 for its first item t0 (a few scalar steps: nl <= 64)
 		const int64_t t0 = t - (threadIdx.x & 63);
@@ -912,11 +920,11 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		return mk(cur.hdx[h], cur.hdy[h], cur.hdz[h]);
 	};
-	unsigned long long verdicts = 0;  // B.fused: bit j = the j-th light's verdict
+	unsigned long long verdicts = 0;  // fused: bit j = the j-th light's verdict
 	for (int j = j0; j < j1; j++) {
 		const bool v = light_verdict<kPacket, kMesh>(S, j, P, n_of, inside, zero_mat, on, d_of, stack, ctr, stats, ws);
 		// light-major: a wave writes 64 adjacent bytes; a zero-term light is skipped by k_shade
-		if (B.fused) {
+		if (fused) {
 			verdicts |= static_cast<unsigned long long>(v) << j;
 		} else if (on) {
 			const auto& cur = *uniform_ptr(opaque(levels) + level);
@@ -930,11 +938,10 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 	// searches only, whose registers leave room for them: 127 VGPRs without spills; the
 	// sphere-only kernel, built for 5 waves, would spill 18)
 	// (with LBVH searches it would spill 26 VGPRs; measured neutral on the batch and C3)
-	constexpr bool kLaneFuse = kMesh == kMeshLinear;
 #if RT_DIAG_LANES
-	if (!kPacket && kLaneFuse && B.fused) diag_lanes(28, on);  // [28] wave slots, [29] lanes shading in place
+	if (!kPacket && fused) diag_lanes(28, on);  // [28] wave slots, [29] lanes shading in place
 #endif
-	if ((kPacket || kLaneFuse) && B.fused && on) {
+	if (kFuse != 0 && fused && on) {
 		const auto& cur = *uniform_ptr(opaque(levels) + level);
 		shade_hit(S, cur, h, P, n_of(), d_of(), [&](int j) { return static_cast<bool>((verdicts >> j) & 1); },
 		          glibc_pow_data::kLogTab, glibc_pow_data::kExpTab, ctr);
@@ -943,7 +950,7 @@ __device__ __forceinline__ void shadow_item(const DeviceScene& S, const ShadeBat
 
 // Host-counted batches launch one thread per item; device-counted ones a fixed grid that
 // strides over the items (the bound is block-uniform: no lane of a wave leaves early).
-template <bool kPacket, bool kCount, int kMesh>
+template <bool kPacket, bool kCount, int kMesh, int kFuse>
 __global__ void __launch_bounds__(kBlock)
     __attribute__((amdgpu_waves_per_eu(kMesh == kMeshNone && !kPacket ? RT_SPHERE_WAVES : kMesh == kMeshLinear && !kPacket ? RT_LINEAR_WAVES : kPacket ? RT_PACKET_WAVES : RT_TRAVERSAL_WAVES))) k_shadow(DeviceScene S, ShadeBatch B,
                                                                      const RayLevel* levels, DeviceCounters* ctr,
@@ -955,7 +962,7 @@ __global__ void __launch_bounds__(kBlock)
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
 	for (int64_t base = xcd_block() * kBlock; base < total; base += stride) {
 		WT_BEGIN();
-		shadow_item<kPacket, kCount, kMesh>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
+		shadow_item<kPacket, kCount, kMesh, kFuse>(S, B, levels, ctr, stats, base + threadIdx.x, stack, stat_lds);
 		WT_END(3 | kPacket << 4 | B.level[0] << 8, base + (threadIdx.x & ~63));
 	}
 }
@@ -1322,9 +1329,12 @@ hipError_t launch_shadow(const DeviceScene& s, const ShadeBatch& b, const RayLev
 	by_mesh_kind(s, [&](auto m) {
 		constexpr int M = decltype(m)::value;
 		if (shadow_packet(b, packet_mask))
-			s.work_stats ? go(k_shadow<true, true, M>) : go(k_shadow<true, false, M>);
+			b.fused ? (s.work_stats ? go(k_shadow<true, true, M, 1>) : go(k_shadow<true, false, M, 1>))
+			        : (s.work_stats ? go(k_shadow<true, true, M, 2>) : go(k_shadow<true, false, M, 2>));
+		else if constexpr (M == kMeshLinear)  // (per lane, fused only without LBVH searches: shadow_can_fuse)
+			s.work_stats ? go(k_shadow<false, true, M, 2>) : go(k_shadow<false, false, M, 2>);
 		else
-			s.work_stats ? go(k_shadow<false, true, M>) : go(k_shadow<false, false, M>);
+			s.work_stats ? go(k_shadow<false, true, M, 0>) : go(k_shadow<false, false, M, 0>);
 	});
 	return hipGetLastError();
 }
