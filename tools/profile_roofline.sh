@@ -1,15 +1,15 @@
 #!/bin/bash
-# Round-4 roofline recipe (the round-3 recipe on the round-4 kernels) (run on the MI355X box via gpurun):
+# Roofline recipe (run on the MI355X box via gpurun):
 #   1. kernel trace + stats of the solo pass (the roofline's time base) and of the default bench
 #   2. HBM bytes: FETCH_SIZE and WRITE_SIZE in separate PMC passes over the solo pass, and the
 #      FETCH_SIZE calibration (tools/fetch_calibration.py)
 #   3. SQ issue/stall counters (+ GRBM_GUI_ACTIVE) over the solo pass, and over the VALU issue
 #      calibration (k_valu_peak: v_fma_f32 / v_pk_fma_f32 / v_fma_f64 at 1-8 waves per SIMD)
-#   usage: tools/profile_round4.sh <tag>
-#   then:  python tools/make_traffic.py gpurun_out/<tag> profiles/round4
-#          python tools/make_valu.py gpurun_out/<tag> profiles/round4
+#   usage: tools/profile_roofline.sh <tag>
+#   then:  python tools/make_traffic.py gpurun_out/<tag> profiles/round<N>
+#          python tools/make_valu.py gpurun_out/<tag> profiles/round<N>
 set -o pipefail
-TAG=${1:-prof4}
+TAG=${1:-prof}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
