@@ -144,7 +144,7 @@ hipError_t clear_device(void* p, size_t bytes) {
 int64_t level_block_bytes(const rt_scene* s, int64_t n) {
 	const int64_t nl = std::max(1, s->ds.n_nonambient);
 	auto align = [](int64_t b) { return (b + 255) & ~int64_t(255); };
-	return 21 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
+	return 18 * align(n * 8) + 4 * align(n * 4) + 2 * align(n) + align(n * nl) + 256;
 }
 
 constexpr int kBudgetMiss = 2;  // internal return code: RTAMD_LEVEL_BUDGET exceeded (render_jobs)
@@ -176,9 +176,9 @@ int alloc_level(rt_scene* s, Lane& ln, size_t level, int64_t capacity) {
 		p += align(b);
 		return r;
 	};
-	double** d[21] = {&L.lv.ox, &L.lv.oy, &L.lv.oz, &L.lv.dx,  &L.lv.dy,  &L.lv.dz,  &L.lv.hpx,
-	                  &L.lv.hpy, &L.lv.hpz, &L.lv.hnx, &L.lv.hny, &L.lv.hnz, &L.lv.hdx, &L.lv.hdy,
-	                  &L.lv.hdz, &L.lv.cr,  &L.lv.cg,  &L.lv.cb,  &L.lv.kr,  &L.lv.kg,  &L.lv.kb};
+	double** d[18] = {&L.lv.ox,  &L.lv.oy,  &L.lv.oz,  &L.lv.dx,  &L.lv.dy,  &L.lv.dz,
+	                  &L.lv.hpx, &L.lv.hpy, &L.lv.hpz, &L.lv.hnx, &L.lv.hny, &L.lv.hnz,
+	                  &L.lv.hdx, &L.lv.hdy, &L.lv.hdz, &L.lv.cr,  &L.lv.cg,  &L.lv.cb};
 	for (double** q : d) *q = reinterpret_cast<double*>(take(n * 8));
 	L.lv.hgeom = reinterpret_cast<int32_t*>(take(n * 4));
 	L.lv.hit_list = reinterpret_cast<int32_t*>(take(n * 4));
@@ -525,10 +525,10 @@ struct Render {
 			}
 			if (nlev > 1) {
 				for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
-					step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1,
+					step(rtamd::launch_reduce_level(s->ds, std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1,
 					                                ln.levels[l].lv, ln.levels[l + 1].lv, st));
 				if (rc == RT_OK)
-					step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, &ln.levels[1].lv, s->stats, st, s->ctr,
+					step(rtamd::launch_output(s->ds, ln.n0, ln.fg, ln.levels[0].lv, &ln.levels[1].lv, s->stats, st, s->ctr,
 					                          finish_on(ln.n0, 256) ? &fin : nullptr));
 			}
 			for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
@@ -614,10 +614,10 @@ struct Render {
 		for (const auto& j : joins)
 			if (rc == RT_OK) step(hipStreamWaitEvent(st, j.first, 0));
 		for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
-			step(rtamd::launch_reduce_level(std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1, ln.levels[l].lv,
+			step(rtamd::launch_reduce_level(s->ds, std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1, ln.levels[l].lv,
 			                                ln.levels[l + 1].lv, st));
 		if (rc == RT_OK)
-			step(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
+			step(rtamd::launch_output(s->ds, ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
 			                          st, s->ctr, finish_on(ln.n0, 256) ? &fin : nullptr));
 		for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
 		return rc;
@@ -786,9 +786,9 @@ struct Render {
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
 		// colours reduced bottom-up; level 0's reduction is fused into the output
 		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 1; l--)
-			HIP_TRY(rtamd::launch_reduce_level(ln.level_n[l], nullptr, ln.levels[l].lv, ln.levels[l + 1].lv,
+			HIP_TRY(rtamd::launch_reduce_level(s->ds, ln.level_n[l], nullptr, ln.levels[l].lv, ln.levels[l + 1].lv,
 			                                   ln.stream));
-		HIP_TRY(rtamd::launch_output(ln.n0, ln.fg, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
+		HIP_TRY(rtamd::launch_output(s->ds, ln.n0, ln.fg, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
 		                             s->stats, ln.stream, s->ctr));
 		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
 		ln.phase = Lane::FINISHING;

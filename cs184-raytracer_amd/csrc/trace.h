@@ -46,7 +46,8 @@ struct RayLevel {
 	uint8_t* occl;               // [non-ambient light][hit] shadow verdicts (light j at j * capacity)
 	// node out
 	double *cr, *cg, *cb;        // local colour, overwritten with the final colour by reduce
-	double *kr, *kg, *kb;        // reflective weight (after TIR), valid when child_refl >= 0
+	// (the reflective weight of a hit with a reflection child is its material's, or 1 on total
+	// internal reflection: reduce_colour derives it from hgeom and child_refr, trace.hip)
 	int32_t *child_refr, *child_refl;
 	int32_t* counts;             // [0] hits of this level (k_closest), [1] children spawned
 	int64_t capacity;
@@ -171,8 +172,8 @@ hipError_t launch_shade(const DeviceScene& s, const ShadeBatch& b, const RayLeve
                         hipStream_t stream);
 // n: the level's ray count, or with n_dev (the previous level's child counter) read on the
 // device (a fixed grid strides over it)
-hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,
-                               hipStream_t stream);
+hipError_t launch_reduce_level(const DeviceScene& s, int64_t n, const int32_t* n_dev, const RayLevel& cur,
+                               const RayLevel& next, hipStream_t stream);
 // Where a fused level (launch_fused) puts its colours: final != 0 (a plan of one traced
 // level): straight into the chunk's output rows (no k_output); else into the level's colours
 // for k_reduce / k_output.  summary != null: the launch's last block reduces the statistics
@@ -186,8 +187,8 @@ struct FusedOut {
 };
 // lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output;
 // pixels go to their rows' outputs (fg.seg); finish non-null: the statistics finish too
-hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
-                         unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr,
+hipError_t launch_output(const DeviceScene& s, int64_t n, const FrameGeometry& fg, const RayLevel& lvl0,
+                         const RayLevel* lvl1, unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr,
                          const FusedOut* finish = nullptr);
 // One level in one launch (k_fused): closest hits, children, and every hit's shadow rays and
 // Phong terms from registers (the level's k_closest + k_shadow + k_shade); never for

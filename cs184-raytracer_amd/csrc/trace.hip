@@ -485,9 +485,7 @@ __device__ __forceinline__ void closest_item(const DeviceScene& S, const FrameGe
 		next.dy[refl_idx] = refl_d.y;
 		next.dz[refl_idx] = refl_d.z;
 		next.inside[refl_idx] = inside;
-		cur.kr[i] = kr[0];
-		cur.kg[i] = kr[1];
-		cur.kb[i] = kr[2];
+		if constexpr (kFused) cur.hgeom[i] = gi;  // for reduce_colour's weight
 	}
 	if (!kFused || !fo->final) {
 		if (active) {
@@ -993,8 +991,13 @@ __global__ void __launch_bounds__(kShadeBlock) k_shade(DeviceScene S, ShadeBatch
 	}
 }
 
-// colour = (local + refraction) + reflection * kr, in place (scene.cpp:127,134)
-__device__ __forceinline__ void reduce_colour(int64_t i, const RayLevel& cur, const RayLevel& next, double c[3]) {
+// colour = (local + refraction) + reflection * kr, in place (scene.cpp:127,134).  kr is the
+// hit material's reflective colour, or 1 on total internal reflection (scene.cpp:119-123):
+// a refractive material's hit with a reflection child and no refraction child is exactly
+// that case (k_closest spawns the refraction child whenever sinT2 <= 1), so kr is derived
+// from the hit geometry instead of being stored per ray (24 B written and read per ray)
+__device__ __forceinline__ void reduce_colour(int64_t i, const RayLevel& cur, const RayLevel& next,
+                                              const DGeom* geoms, const DMaterial* mats, double c[3]) {
 	c[0] = cur.cr[i];
 	c[1] = cur.cg[i];
 	c[2] = cur.cb[i];
@@ -1005,18 +1008,21 @@ __device__ __forceinline__ void reduce_colour(int64_t i, const RayLevel& cur, co
 		c[2] = c[2] + next.cb[t];
 	}
 	if (r >= 0) {
-		c[0] = c[0] + next.cr[r] * cur.kr[i];
-		c[1] = c[1] + next.cg[r] * cur.kg[i];
-		c[2] = c[2] + next.cb[r] * cur.kb[i];
+		const DMaterial& M = mats[geoms[cur.hgeom[i]].mat];
+		const bool tir = M.kt_nonzero && t < 0;
+		c[0] = c[0] + next.cr[r] * (tir ? 1.0 : M.kr[0]);
+		c[1] = c[1] + next.cg[r] * (tir ? 1.0 : M.kr[1]);
+		c[2] = c[2] + next.cb[r] * (tir ? 1.0 : M.kr[2]);
 	}
 }
-__global__ void k_reduce(int64_t n_host, const int32_t* n_dev, RayLevel cur, RayLevel next) {
+__global__ void k_reduce(int64_t n_host, const int32_t* n_dev, RayLevel cur, RayLevel next, const DGeom* geoms,
+                         const DMaterial* mats) {
 	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur.capacity) : n_host;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
 	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
 		if (cur.child_refr[i] < 0 && cur.child_refl[i] < 0) continue;
 		double c[3];
-		reduce_colour(i, cur, next, c);
+		reduce_colour(i, cur, next, geoms, mats, c);
 		cur.cr[i] = c[0];
 		cur.cg[i] = c[1];
 		cur.cb[i] = c[2];
@@ -1025,8 +1031,8 @@ __global__ void k_reduce(int64_t n_host, const int32_t* n_dev, RayLevel cur, Ray
 
 // the image: level 0's colours, reduced with level 1 on the fly when `reduce` (the last
 // k_reduce fused into the output); fo.summary: the last block finishes the statistics
-__global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lvl1, int32_t reduce,
-                         unsigned long long* stats, DeviceCounters* ctr, FusedOut fo) {
+__global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lvl1, int32_t reduce, const DGeom* geoms,
+                         const DMaterial* mats, unsigned long long* stats, DeviceCounters* ctr, FusedOut fo) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const int32_t io = fg.intersection_only;
 	// level 0's counts were read back; clear them for the lane's next chunk
@@ -1034,7 +1040,7 @@ __global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lv
 	double v[3] = {0, 0, 0};
 	if (i < n) {
 		if (reduce) {
-			reduce_colour(i, lvl0, lvl1, v);
+			reduce_colour(i, lvl0, lvl1, geoms, mats, v);
 		} else {
 			v[0] = lvl0.cr[i];
 			v[1] = lvl0.cg[i];
@@ -1348,20 +1354,21 @@ hipError_t launch_shade(const DeviceScene& s, const ShadeBatch& b, const RayLeve
 	return hipGetLastError();
 }
 
-hipError_t launch_reduce_level(int64_t n, const int32_t* n_dev, const RayLevel& cur, const RayLevel& next,
-                               hipStream_t stream) {
+hipError_t launch_reduce_level(const DeviceScene& s, int64_t n, const int32_t* n_dev, const RayLevel& cur,
+                               const RayLevel& next, hipStream_t stream) {
 	if (n <= 0) return hipSuccess;
 	const unsigned grid = n_dev ? dev_grid(n, 256) : grid_for(n, 256);
-	hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, stream, n, n_dev, cur, next);
+	hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, stream, n, n_dev, cur, next, s.geoms, s.mats);
 	return hipGetLastError();
 }
 
-hipError_t launch_output(int64_t n, const FrameGeometry& fg, const RayLevel& lvl0, const RayLevel* lvl1,
-                         unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr, const FusedOut* finish) {
+hipError_t launch_output(const DeviceScene& s, int64_t n, const FrameGeometry& fg, const RayLevel& lvl0,
+                         const RayLevel* lvl1, unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr,
+                         const FusedOut* finish) {
 	if (n <= 0) return hipSuccess;
 	const FusedOut fo = finish ? *finish : FusedOut{};
 	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, fg, lvl0, lvl1 ? *lvl1 : lvl0,
-	                   lvl1 ? 1 : 0, stats, ctr, fo);
+	                   lvl1 ? 1 : 0, s.geoms, s.mats, stats, ctr, fo);
 	return hipGetLastError();
 }
 
