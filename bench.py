@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--sweep", default="C5_refraction3_4096_bd8,C4_airboat_sub_1920x1080",
                     help="configs whose single frame is row-partitioned over 1, 2, 4, 8 ranks ('' = none)")
     ap.add_argument("--sweep-reps", type=int, default=3)
+    ap.add_argument("--step-order", action="store_true",
+                    help="partition mode: hand each rank's frames to the batch call in step order "
+                         "instead of rtamd.dist.batch_order (the A/B control)")
     ap.add_argument("--solo-frames", type=int, default=4,
                     help="frames rendered (one batch call) with every kernel alone (RTAMD_SERIAL=1) for the roofline "
                          "time base")
@@ -541,6 +544,8 @@ def emulated_batch_partition(a, s, W, H, kw, blk, cfg, torch, n=8):
     bblk = a.batch_block if a.batch_block > 0 else rd.band_rows(H, n)
     for k in range(n):  # rank k's rotated share (rtamd.dist.batch_rows), as bench.py's partition step renders it
         sel = rd.batch_rows(H, k, n, F, bblk)
+        if not a.step_order:
+            sel = [sel[f] for f in rd.batch_order(k, n, F)]
         rows = max(rd.n_rows(H, q, n, bblk) for q in range(n))
         ms, r = timed([s.params(W, H, kw["bdepth"], kw["intersection_only"], b, e, st, row_block=bl)
                        for (b, e, st, bl) in sel], rows)
@@ -728,6 +733,10 @@ def main():
     comm = torch.cuda.Stream() if world > 1 else torch.cuda.current_stream()
     prms = [s.params(W, H, kw["bdepth"], kw["intersection_only"], r[0], r[1], r[2], row_block=r[3]) for r in frame_rows]
     prm = prms[0]
+    # the frames in the order the rank hands them to the batch call (rtamd.dist.batch_order:
+    # every rank's chunks hold the image's blocks in the same order); outputs stay per frame
+    order = rd.batch_order(rank, ways, B) if partition and not a.step_order else list(range(B))
+    prms_ordered = [prms[f] for f in order]
     stream = torch.cuda.current_stream().cuda_stream
     gbufs = torch.empty((world, B, n_buf, W, 3), dtype=torch.uint8, device="cuda") \
         if rank == 0 and world > 1 and partition else None
@@ -743,8 +752,8 @@ def main():
         n_steps[0] += 1
         if gathered[k] is not None:  # the gathers that read these buffers two steps ago
             torch.cuda.current_stream().wait_event(gathered[k])
-        st = s.render_batch_device(prms, [o.data_ptr() for o in outs], [out8s[k][f].data_ptr() for f in range(B)],
-                                   stream)
+        st = s.render_batch_device(prms_ordered, [outs[f].data_ptr() for f in order],
+                                   [out8s[k][f].data_ptr() for f in order], stream)
         rendered = torch.cuda.Event()
         rendered.record()
         with torch.cuda.stream(comm):

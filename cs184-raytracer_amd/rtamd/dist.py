@@ -112,6 +112,21 @@ def batch_rows(height: int, rank: int, world: int, frames: int, block: int = 1, 
     return [rank_rows(height, rank, world, shift=(f % world) if rotate else 0, block=block) for f in range(frames)]
 
 
+def batch_order(rank: int, world: int, frames: int) -> list:
+    """The order in which a rank hands its frames of a rotated batch (batch_rows) to one
+    rt_render_batch_device call: within each cycle of `world` frames, by the residue of the
+    blocks the rank renders, so that every rank's chunks hold the image's blocks in the same
+    order (0, 1, ..., world - 1) and take the same time.  (Each frame keeps its own output
+    rows, so the order changes neither the images nor the gather; measured: with frames in
+    step order the ranks whose chunks start mid-image were up to 20% slower, bench.py
+    --sweep, profiles/round6/ab/README.md.)"""
+    order = []
+    for c in range(0, frames, world):
+        cyc = [f for f in range(c, min(c + world, frames))]
+        order += sorted(cyc, key=lambda f: (rank + f) % world)
+    return order
+
+
 def gather_rows_batch(local: torch.Tensor, height: int, dst: int = 0, out: Optional[torch.Tensor] = None,
                       bufs: Optional[torch.Tensor] = None, block: int = 1,
                       rotate: bool = False) -> Optional[torch.Tensor]:

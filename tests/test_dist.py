@@ -194,3 +194,22 @@ def test_single_rank_frame_is_the_single_render(oracle, io):
         return torch.from_numpy(img), 7.0
     frame = rd.render_frame(render_rows, h, io, torch.device("cpu"), block=8)
     assert np.array_equal(frame.numpy(), want)
+
+
+@pytest.mark.parametrize("world,frames", [(1, 5), (2, 4), (3, 7), (8, 48), (8, 3)])
+def test_batch_order_puts_every_rank_blocks_in_one_order(world, frames):
+    """bench.py hands each rank's frames of a rotated batch to the batch call in
+    rtamd.dist.batch_order: a permutation of the step's frames, cycle by cycle, under which
+    every rank renders the image's blocks in the order 0, 1, ..., world - 1 (so all ranks'
+    chunks hold the same block sequence)."""
+    from rtamd import dist as rd
+    for rank in range(world):
+        order = rd.batch_order(rank, world, frames)
+        assert sorted(order) == list(range(frames))
+        for c in range(0, frames, world):
+            cyc = order[c:c + world]
+            assert sorted(cyc) == list(range(c, min(c + world, frames)))
+            residues = [(rank + f) % world for f in cyc]
+            assert residues == sorted(residues)
+            if len(cyc) == world:
+                assert residues == list(range(world))
