@@ -3,7 +3,7 @@ call in a given band order (jobs of one frame's row range each, outputs at the b
 does the order in which a chunk holds the image's rows change the rate?  (round 6: the
 8-way shares of bench.py's partition, profiles/round6/ab/README.md)
 
-usage: python tools/order_probe.py <config> [frames] [reps]"""
+usage: python tools/order_probe.py <config> [frames] [reps] [order,order,...]"""
 import os
 import sys
 import time
@@ -30,6 +30,8 @@ stream = torch.cuda.current_stream().cuda_stream
 orders = {"whole": None, "natural": list(range(n)), "shift4": [4, 5, 6, 7, 0, 1, 2, 3],
           "reverse": list(range(n - 1, -1, -1)), "interleave": [0, 4, 1, 5, 2, 6, 3, 7],
           "outside_in": [0, 7, 1, 6, 2, 5, 3, 4], "middle_out": [3, 4, 2, 5, 1, 6, 0, 7]}
+if len(sys.argv) > 4:
+    orders = {k: orders[k] for k in sys.argv[4].split(",")}
 res = {}
 for rnd in range(2):
     for tag, order in orders.items():
