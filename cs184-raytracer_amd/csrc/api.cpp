@@ -523,14 +523,8 @@ struct Render {
 				                         L == nlev - 1 && remaining > 0, fo));
 				launches[0]++;
 			}
-			if (nlev > 1) {
-				for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
-					step(rtamd::launch_reduce_level(s->ds, std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1,
-					                                ln.levels[l].lv, ln.levels[l + 1].lv, st));
-				if (rc == RT_OK)
-					step(rtamd::launch_output(s->ds, ln.n0, ln.fg, ln.levels[0].lv, &ln.levels[1].lv, s->stats, st, s->ctr,
-					                          finish_on(ln.n0, 256) ? &fin : nullptr));
-			}
+			if (nlev > 1 && rc == RT_OK)
+				step(reduce_and_output(ln, nlev, pl.level_n, true, st, finish_on(ln.n0, 256) ? &fin : nullptr));
 			for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
 			return rc;
 		}
@@ -613,12 +607,7 @@ struct Render {
 		}
 		for (const auto& j : joins)
 			if (rc == RT_OK) step(hipStreamWaitEvent(st, j.first, 0));
-		for (int l = nlev - 2; l >= 1 && rc == RT_OK; l--)
-			step(rtamd::launch_reduce_level(s->ds, std::max<int64_t>(pl.level_n[l], 1), ln.levels[l - 1].lv.counts + 1, ln.levels[l].lv,
-			                                ln.levels[l + 1].lv, st));
-		if (rc == RT_OK)
-			step(rtamd::launch_output(s->ds, ln.n0, ln.fg, ln.levels[0].lv, nlev > 1 ? &ln.levels[1].lv : nullptr, s->stats,
-			                          st, s->ctr, finish_on(ln.n0, 256) ? &fin : nullptr));
+		if (rc == RT_OK) step(reduce_and_output(ln, nlev, pl.level_n, true, st, finish_on(ln.n0, 256) ? &fin : nullptr));
 		for (int k = 0; k < 3; k++) pl.launches[k] = launches[k];
 		return rc;
 	}
@@ -664,6 +653,27 @@ struct Render {
 			return &ln.plans.back();
 		}
 		return nullptr;
+	}
+
+	// The chunk's colours reduced bottom-up, two levels per launch (rtamd::reduce_steps), level
+	// 0's reduction in the output launch.  device_counts: the level sizes are bounds and the
+	// launches read the levels' ray counts on the device (replayed plans)
+	hipError_t reduce_and_output(Lane& ln, int nlev, const std::vector<int64_t>& level_n, bool device_counts,
+	                             hipStream_t st, const rtamd::FusedOut* fin) {
+		std::vector<rtamd::ReduceStep> steps(std::max(1, nlev));
+		const int n = rtamd::reduce_steps(nlev, steps.data());
+		for (int k = 0; k < n; k++) {
+			const int l = steps[k].level, m = steps[k].levels;
+			const rtamd::RayLevel* low = m == 2 ? &ln.levels[l + 2].lv : nullptr;
+			const hipError_t e =
+			    l > 0 ? rtamd::launch_reduce_level(s->ds, device_counts ? std::max<int64_t>(level_n[l], 1) : level_n[l],
+			                                       device_counts ? ln.levels[l - 1].lv.counts + 1 : nullptr, ln.levels[l].lv,
+			                                       ln.levels[l + 1].lv, low, st)
+			          : rtamd::launch_output(s->ds, ln.n0, ln.fg, ln.levels[0].lv, m >= 1 ? &ln.levels[1].lv : nullptr, low,
+			                                 s->stats, st, s->ctr, fin);
+			if (e != hipSuccess) return e;
+		}
+		return hipSuccess;
 	}
 
 	// The chunk's rows as by-value descriptors (FrameGeometry::seg, one per piece: the kernels
@@ -784,12 +794,7 @@ struct Render {
 			if ((rc = launch_shading(ln, {ln.deferred.begin() + k, ln.deferred.begin() + e}, q))) return rc;
 		}
 		for (int first : ln.shaded) HIP_TRY(hipStreamWaitEvent(ln.stream, ln.level_events[first][4], 0));
-		// colours reduced bottom-up; level 0's reduction is fused into the output
-		for (int l = static_cast<int>(ln.level_n.size()) - 2; l >= 1; l--)
-			HIP_TRY(rtamd::launch_reduce_level(s->ds, ln.level_n[l], nullptr, ln.levels[l].lv, ln.levels[l + 1].lv,
-			                                   ln.stream));
-		HIP_TRY(rtamd::launch_output(s->ds, ln.n0, ln.fg, ln.levels[0].lv, ln.level_n.size() > 1 ? &ln.levels[1].lv : nullptr,
-		                             s->stats, ln.stream, s->ctr));
+		HIP_TRY(reduce_and_output(ln, static_cast<int>(ln.level_n.size()), ln.level_n, false, ln.stream, nullptr));
 		HIP_TRY(hipEventRecord(ln.chunk_done, ln.stream));
 		ln.phase = Lane::FINISHING;
 		return RT_OK;

@@ -172,8 +172,10 @@ hipError_t launch_shade(const DeviceScene& s, const ShadeBatch& b, const RayLeve
                         hipStream_t stream);
 // n: the level's ray count, or with n_dev (the previous level's child counter) read on the
 // device (a fixed grid strides over it)
+// low non-null: two levels at once, cur's final colours from next's local colours reduced on
+// the fly with low's final ones (next's final colours are not written)
 hipError_t launch_reduce_level(const DeviceScene& s, int64_t n, const int32_t* n_dev, const RayLevel& cur,
-                               const RayLevel& next, hipStream_t stream);
+                               const RayLevel& next, const RayLevel* low, hipStream_t stream);
 // Where a fused level (launch_fused) puts its colours: final != 0 (a plan of one traced
 // level): straight into the chunk's output rows (no k_output); else into the level's colours
 // for k_reduce / k_output.  summary != null: the launch's last block reduces the statistics
@@ -185,11 +187,24 @@ struct FusedOut {
 	unsigned long long* summary;
 	uint32_t* done;
 };
-// lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output;
-// pixels go to their rows' outputs (fg.seg); finish non-null: the statistics finish too
+// lvl1 non-null: level 0's reduction with level 1 (k_reduce) is fused into the output (lvl2
+// non-null too: with levels 1 and 2, as launch_reduce_level's two-level form); pixels go to
+// their rows' outputs (fg.seg); finish non-null: the statistics finish too
 hipError_t launch_output(const DeviceScene& s, int64_t n, const FrameGeometry& fg, const RayLevel& lvl0,
-                         const RayLevel* lvl1, unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr,
-                         const FusedOut* finish = nullptr);
+                         const RayLevel* lvl1, const RayLevel* lvl2, unsigned long long* stats, hipStream_t stream,
+                         DeviceCounters* ctr, const FusedOut* finish = nullptr);
+// The reductions of a chunk of n_levels traced levels, deepest first, two levels per launch:
+// {l, k} reduces level l with the k levels below it (l = 0: the output launch)
+struct ReduceStep {
+	int level, levels;
+};
+inline int reduce_steps(int n_levels, ReduceStep* out /* n_levels entries */) {
+	int n = 0, j = n_levels - 1;  // j: the deepest level whose colours are final
+	for (; j >= 2; j -= 2) out[n++] = {j - 2, 2};
+	if (j == 1) out[n++] = {0, 1};
+	if (n_levels == 1) out[n++] = {0, 0};
+	return n;
+}
 // One level in one launch (k_fused): closest hits, children, and every hit's shadow rays and
 // Phong terms from registers (the level's k_closest + k_shadow + k_shade); never for
 // --intersection-only or counting renders.  Arguments as launch_closest.

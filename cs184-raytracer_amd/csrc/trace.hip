@@ -1015,23 +1015,57 @@ __device__ __forceinline__ void reduce_colour(int64_t i, const RayLevel& cur, co
 		c[2] = c[2] + next.cb[r] * (tir ? 1.0 : M.kr[2]);
 	}
 }
-__global__ void k_reduce(int64_t n_host, const int32_t* n_dev, RayLevel cur, RayLevel next, const DGeom* geoms,
-                         const DMaterial* mats) {
+// Two levels in one pass: cur's final colour from next's colours reduced on the fly with
+// low's final ones (reduce_colour of each child, in registers): the same operations in the
+// same order as reducing next in a launch of its own and then cur, without writing next's
+// final colours (nothing else reads them) or a launch between the two
+__device__ __forceinline__ void reduce_colour2(int64_t i, const RayLevel& cur, const RayLevel& next, const RayLevel& low,
+                                               const DGeom* geoms, const DMaterial* mats, double c[3]) {
+	c[0] = cur.cr[i];
+	c[1] = cur.cg[i];
+	c[2] = cur.cb[i];
+	const int32_t t = cur.child_refr[i], r = cur.child_refl[i];
+	if (t >= 0) {
+		double m[3];
+		reduce_colour(t, next, low, geoms, mats, m);
+		c[0] = c[0] + m[0];
+		c[1] = c[1] + m[1];
+		c[2] = c[2] + m[2];
+	}
+	if (r >= 0) {
+		double m[3];
+		reduce_colour(r, next, low, geoms, mats, m);
+		const DMaterial& M = mats[geoms[cur.hgeom[i]].mat];
+		const bool tir = M.kt_nonzero && t < 0;
+		c[0] = c[0] + m[0] * (tir ? 1.0 : M.kr[0]);
+		c[1] = c[1] + m[1] * (tir ? 1.0 : M.kr[1]);
+		c[2] = c[2] + m[2] * (tir ? 1.0 : M.kr[2]);
+	}
+}
+// kLevels 1: cur's final colours from next's; 2: from next's and low's (reduce_colour2)
+template <int kLevels>
+__global__ void k_reduce(int64_t n_host, const int32_t* n_dev, RayLevel cur, RayLevel next, RayLevel low,
+                         const DGeom* geoms, const DMaterial* mats) {
 	const int64_t n = n_dev ? min(static_cast<int64_t>(*n_dev), cur.capacity) : n_host;
 	const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
 	for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
 		if (cur.child_refr[i] < 0 && cur.child_refl[i] < 0) continue;
 		double c[3];
-		reduce_colour(i, cur, next, geoms, mats, c);
+		if constexpr (kLevels == 2)
+			reduce_colour2(i, cur, next, low, geoms, mats, c);
+		else
+			reduce_colour(i, cur, next, geoms, mats, c);
 		cur.cr[i] = c[0];
 		cur.cg[i] = c[1];
 		cur.cb[i] = c[2];
 	}
 }
 
-// the image: level 0's colours, reduced with level 1 on the fly when `reduce` (the last
-// k_reduce fused into the output); fo.summary: the last block finishes the statistics
-__global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lvl1, int32_t reduce, const DGeom* geoms,
+// the image: level 0's colours, reduced on the fly with level 1 (kReduce 1: the last k_reduce
+// fused into the output) or with levels 1 and 2 (kReduce 2, reduce_colour2); fo.summary: the
+// last block finishes the statistics
+template <int kReduce>
+__global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lvl1, RayLevel lvl2, const DGeom* geoms,
                          const DMaterial* mats, unsigned long long* stats, DeviceCounters* ctr, FusedOut fo) {
 	const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
 	const int32_t io = fg.intersection_only;
@@ -1039,7 +1073,9 @@ __global__ void k_output(int64_t n, FrameGeometry fg, RayLevel lvl0, RayLevel lv
 	if (i == 0) lvl0.counts[0] = lvl0.counts[1] = 0;
 	double v[3] = {0, 0, 0};
 	if (i < n) {
-		if (reduce) {
+		if constexpr (kReduce == 2) {
+			reduce_colour2(i, lvl0, lvl1, lvl2, geoms, mats, v);
+		} else if constexpr (kReduce == 1) {
 			reduce_colour(i, lvl0, lvl1, geoms, mats, v);
 		} else {
 			v[0] = lvl0.cr[i];
@@ -1355,20 +1391,33 @@ hipError_t launch_shade(const DeviceScene& s, const ShadeBatch& b, const RayLeve
 }
 
 hipError_t launch_reduce_level(const DeviceScene& s, int64_t n, const int32_t* n_dev, const RayLevel& cur,
-                               const RayLevel& next, hipStream_t stream) {
+                               const RayLevel& next, const RayLevel* low, hipStream_t stream) {
 	if (n <= 0) return hipSuccess;
 	const unsigned grid = n_dev ? dev_grid(n, 256) : grid_for(n, 256);
-	hipLaunchKernelGGL(k_reduce, dim3(grid), dim3(256), 0, stream, n, n_dev, cur, next, s.geoms, s.mats);
+	if (low)
+		hipLaunchKernelGGL(k_reduce<2>, dim3(grid), dim3(256), 0, stream, n, n_dev, cur, next, *low, s.geoms, s.mats);
+	else
+		hipLaunchKernelGGL(k_reduce<1>, dim3(grid), dim3(256), 0, stream, n, n_dev, cur, next, next, s.geoms, s.mats);
 	return hipGetLastError();
 }
 
 hipError_t launch_output(const DeviceScene& s, int64_t n, const FrameGeometry& fg, const RayLevel& lvl0,
-                         const RayLevel* lvl1, unsigned long long* stats, hipStream_t stream, DeviceCounters* ctr,
-                         const FusedOut* finish) {
+                         const RayLevel* lvl1, const RayLevel* lvl2, unsigned long long* stats, hipStream_t stream,
+                         DeviceCounters* ctr, const FusedOut* finish) {
 	if (n <= 0) return hipSuccess;
 	const FusedOut fo = finish ? *finish : FusedOut{};
-	hipLaunchKernelGGL(k_output, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, fg, lvl0, lvl1 ? *lvl1 : lvl0,
-	                   lvl1 ? 1 : 0, s.geoms, s.mats, stats, ctr, fo);
+	const RayLevel& l1 = lvl1 ? *lvl1 : lvl0;
+	const RayLevel& l2 = lvl2 ? *lvl2 : l1;
+	auto go = [&](auto kernel) {
+		hipLaunchKernelGGL(kernel, dim3(grid_for(n, 256)), dim3(256), 0, stream, n, fg, lvl0, l1, l2, s.geoms, s.mats,
+		                   stats, ctr, fo);
+	};
+	if (lvl1 && lvl2)
+		go(k_output<2>);
+	else if (lvl1)
+		go(k_output<1>);
+	else
+		go(k_output<0>);
 	return hipGetLastError();
 }
 
