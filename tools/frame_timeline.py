@@ -8,12 +8,12 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 
 
 def name(r):
-    m = re.search(r"(k_[a-z0-9_]+(?:<[a-z, ]+>)?)\(", r["Kernel_Name"])
+    m = re.search(r"(k_[a-z0-9_]+(?:<[a-z0-9, ]+>)?)\(", r["Kernel_Name"])
     return m.group(1) if m else r["Kernel_Name"][:20]
 
 
 names = [name(r) for r in rows]
-outs = [i for i, n in enumerate(names) if n == "k_output"]
+outs = [i for i, n in enumerate(names) if n.startswith("k_output")]
 a, b = outs[-2] + 1, outs[-1]
 t0 = int(rows[a]["Start_Timestamp"])
 busy = 0
