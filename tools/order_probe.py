@@ -30,6 +30,24 @@ stream = torch.cuda.current_stream().cuda_stream
 orders = {"whole": None, "natural": list(range(n)), "shift4": [4, 5, 6, 7, 0, 1, 2, 3],
           "reverse": list(range(n - 1, -1, -1)), "interleave": [0, 4, 1, 5, 2, 6, 3, 7],
           "outside_in": [0, 7, 1, 6, 2, 5, 3, 4], "middle_out": [3, 4, 2, 5, 1, 6, 0, 7]}
+# per-band cost: every frame's band k alone (48 jobs of one band), ms per call
+band_ms = []
+for k in range(n):
+    b, e = bands[k]
+    prms = [s.params(W, H, kw["bdepth"], kw["intersection_only"], b, e, 1)] * F
+    ptrs = [out8[f, b].data_ptr() for f in range(F)]
+    ts = []
+    for rep in range(4):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.render_batch_device(prms, [], ptrs, stream)
+        torch.cuda.synchronize()
+        if rep:
+            ts.append(time.perf_counter() - t0)
+    band_ms.append(round(sorted(ts)[len(ts) // 2] * 1e3, 3))
+print(name, "band ms", band_ms, flush=True)
+orders["lpt"] = sorted(range(n), key=lambda k: -band_ms[k])     # most expensive first
+orders["spt"] = sorted(range(n), key=lambda k: band_ms[k])      # cheapest first
 if len(sys.argv) > 4:
     orders = {k: orders[k] for k in sys.argv[4].split(",")}
 res = {}
