@@ -93,8 +93,11 @@ def parse():
                          "time base")
     ap.add_argument("--solo-only", action="store_true",
                     help="run only the solo pass (the command rocprofv3 profiles for the roofline)")
-    ap.add_argument("--latency-frames", type=int, default=11,
-                    help="single-frame renders timed after the run (wall-clock latency of one frame)")
+    ap.add_argument("--latency-frames", type=int, default=21,
+                    help="single-frame renders timed after the run (wall-clock latency of one frame; median)")
+    ap.add_argument("--latency-warmup", type=int, default=2,
+                    help="single-frame renders before those, not timed: the first render of the frame's shape "
+                         "is traced host-driven and builds its launch plan (api.cpp)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample length")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None,
@@ -807,6 +810,8 @@ def main():
         parity["frame"] = f"frame {n_frames_rank0 - 1} of the last timed step (buffer set {last})"
     # wall-clock of ONE frame's rows on this rank (one render call, nothing else in flight)
     lat = []
+    for _ in range(max(0, a.latency_warmup) if a.latency_frames > 0 else 0):
+        s.render_device(prm, outs[0].data_ptr(), out8s[0][0].data_ptr(), stream)
     for _ in range(max(0, a.latency_frames)):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
@@ -866,6 +871,8 @@ def main():
                        "rays_per_frame": int(rays / a.steps / fps),
                        "ms_per_frame": round(elapsed / a.steps / fps * 1e3, 3),
                        "frame_latency_ms": round(latency * 1e3, 3),
+                       "frame_latency_how": f"median of {a.latency_frames} single-frame render_device calls (f64 + RGB8 "
+                                            f"into HBM) after the timed steps and {a.latency_warmup} untimed ones",
                        "row_block": blk if partition else None,
                        "parallelism": (f"EMULATED rank share: rank 0's {n_loc:g} of {H} rows per frame of an {ways}-way "
                                        f"partition, {fps} frames/step on 1 GPU (development measure, not a job)"
