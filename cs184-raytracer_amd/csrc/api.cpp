@@ -1117,7 +1117,7 @@ int scene_create(const rtamd::Scene& scene, int device, rt_scene** out) {
 	// tuning knobs; lanes are created on first use
 	if (const char* pm = std::getenv("RTAMD_PACKET_MASK")) s->packet_mask = std::atoi(pm);
 	if (const char* dl = std::getenv("RTAMD_DIRECT_LEVELS"))
-		s->direct_levels_single = s->direct_levels_batch = std::max(1, std::atoi(dl));
+		s->direct_levels_single = s->direct_levels_two_lanes = s->direct_levels_batch = std::max(1, std::atoi(dl));
 	if (const char* nl = std::getenv("RTAMD_LANES")) s->single_lanes = std::min(kMaxLanes, std::max(0, std::atoi(nl)));
 	if (const char* bl = std::getenv("RTAMD_BATCH_LANES"))
 		s->batch_lanes = std::min(kMaxLanes, std::max(1, std::atoi(bl)));
@@ -1527,7 +1527,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	int rc = ensure_lanes(s, n_lanes, minimal);
 	if (rc) return rc;
 	Render R{s};
-	R.direct_levels = batch ? s->direct_levels_batch : s->direct_levels_single;
+	R.direct_levels = batch ? s->direct_levels_batch : n_lanes > 1 ? s->direct_levels_two_lanes : s->direct_levels_single;
 	R.deep_split = batch ? s->deep_split_batch : s->deep_split_single;
 	R.light_major_below = batch ? s->light_major_below_batch : s->light_major_below_single;
 	R.progress = progress;

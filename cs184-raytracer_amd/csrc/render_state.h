@@ -178,8 +178,12 @@ struct rt_scene {
 	// RTAMD_DIRECT_LEVELS: levels shaded beside the closest-hit chain; the rest are shaded in
 	// batches after it.  Measured best on C3: 3 for one frame per call
 	// (latency: level 1's shading overlaps levels 2+), 1 for batches (throughput: fewer,
-	// larger shading launches while other frames fill the GPU).  The variable sets both.
+	// larger shading launches while other frames fill the GPU).  A frame of more than one chunk,
+	// traced by two lanes (single_lanes auto), takes 2: each lane's chain then shares the GPU
+	// with the other lane's shading as well (round 6: C5 -2.9%, bunny and al at 4096^2 -3% and
+	// -9%, al at 2896^2 -5%; one-chunk frames lose 1-3% with 2).  The variable sets all three.
 	int direct_levels_single = 3;
+	int direct_levels_two_lanes = 2;
 	int direct_levels_batch = 1;
 	int single_lanes = 0;                        // lanes one frame is split over (RTAMD_LANES); 0 = auto
 	// chunk pipelines of a batch in flight (RTAMD_BATCH_LANES).  4 lanes gave the C3 bench

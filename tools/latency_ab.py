@@ -2,7 +2,7 @@
 variants (each variant in its own process, since the library reads its knobs at scene
 creation), rounds alternating on one box.
 
-usage: python tools/latency_ab.py <rounds> <config[@k/n][,config...]> [VAR=V[,VAR=V]] ...
+usage: python tools/latency_ab.py <rounds> <config|scene.rti[:WxH][+bdN][@k/n][,...]> [VAR=V[,VAR=V]] ...
        (the first variant is always the default environment)"""
 import json
 import os
@@ -20,8 +20,18 @@ from rtamd.configs import CONFIGS, SCENES, option_kwargs
 res = {}
 for name in sys.argv[1].split(","):
     cfg, _, share = name.partition("@")
-    scene, w, h, flags = CONFIGS[cfg]
+    cfg, _, bd = cfg.partition("+bd")  # +bdN: another bounce depth
+    cfg, _, size = cfg.partition(":")  # cfg:WxH renders the config's scene and options at another size
+    if cfg.endswith(".rti"):  # a shipped scene by file name (excess_inputs/ or inputs/), 1024^2, depth 10
+        sub = "excess_inputs" if os.path.exists(os.path.join(SCENES, "excess_inputs", cfg)) else "inputs"
+        scene, w, h, flags = os.path.join(sub, cfg), 1024, 1024, []
+    else:
+        scene, w, h, flags = CONFIGS[cfg]
+    if size:
+        w, h = (int(v) for v in size.split("x"))
     kw = option_kwargs(flags)
+    if bd:
+        kw["bdepth"] = int(bd)
     s = rtamd.load_scene(os.path.join(SCENES, scene))
     out = torch.empty((h, w, 3), dtype=torch.float64, device="cuda")
     out8 = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
