@@ -1529,7 +1529,7 @@ int render_jobs_impl(rt_scene* s, std::vector<Job>& jobs, hipStream_t caller, rt
 	Render R{s};
 	R.direct_levels = batch ? s->direct_levels_batch : n_lanes > 1 ? s->direct_levels_two_lanes : s->direct_levels_single;
 	R.deep_split = batch ? s->deep_split_batch : s->deep_split_single;
-	R.light_major_below = batch ? s->light_major_below_batch : s->light_major_below_single;
+	R.light_major_below = batch || n_lanes > 1 ? s->light_major_below_batch : s->light_major_below_single;
 	R.progress = progress;
 	R.cnt.intersection_max = 2.2250738585072014e-308;  // numeric_limits<double>::min() (scene.cpp:51)
 	// the caller's stream is joined first (its prior work, e.g. the allocation of the

@@ -214,6 +214,9 @@ struct rt_scene {
 	// C3 1.284 -> 1.259),
 	// a batch below 128 K (its level-1 launch of 2-frame chunks, ~840 K hits, measured -7% as
 	// light-major, and an 8-way row share -3 to -6%: DESIGN.md §4)
+	// A frame traced by two lanes (more than one chunk) takes the batch's threshold: its
+	// launches have the batch's size (round 6: al at 2896^2 / 4096^2 -3.4% / -2.6%, the bunny
+	// at 4096^2 -0.5%)
 	int64_t light_major_below_single = (int64_t)1 << 20;
 	int64_t light_major_below_batch = (int64_t)1 << 17;
 	// RTAMD_ONE_STREAM_PIXELS: a replayed chunk of at most this many pixels is issued on one
